@@ -1,0 +1,118 @@
+"""ctypes binding of include/ecgpu.h (libecgpu.so).
+
+Loaded strictly from the in-tree build (erasure_coding_test_amd/lib/).  There
+is no fallback: if the library is missing the import fails with instructions
+to run the build.  ``torch`` is imported first on purpose -- the PyTorch-ROCm
+wheel ships its own HIP runtime (soname libamdhip64.so.7); loading it first
+makes libecgpu bind to that same runtime, so device pointers and streams from
+torch tensors are valid in our kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module doc)
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libecgpu.so")
+DROPIN_PATH = os.path.join(LIB_DIR, "libjerasure_amd.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build the HIP extension first "
+        "(python erasure_coding_test_amd/build.py, or __graft_entry__.build())")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+c_int, c_int64, c_void_p, c_char_p = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_char_p
+c_int_p = ctypes.POINTER(ctypes.c_int)
+c_void_pp = ctypes.POINTER(ctypes.c_void_p)
+c_double_p = ctypes.POINTER(ctypes.c_double)
+
+ECGPU_OK, ECGPU_ERR, ECGPU_ERR_ARG, ECGPU_ERR_HIP, ECGPU_ERR_NOMEM = 0, -1, -2, -3, -4
+KERNEL_PERM, KERNEL_LDS = 0, 1
+
+# name -> (restype, argtypes); kept in step with include/ecgpu.h (tests check
+# that every declared symbol is exported).
+SIGNATURES = {
+    "ecgpu_version": (c_char_p, []),
+    "ecgpu_last_error": (c_char_p, []),
+    "ecgpu_free": (None, [c_void_p]),
+    "ecgpu_galois_single_multiply": (c_int, [c_int, c_int, c_int]),
+    "ecgpu_galois_single_divide": (c_int, [c_int, c_int, c_int]),
+    "ecgpu_galois_inverse": (c_int, [c_int, c_int]),
+    "ecgpu_galois_log": (c_int, [c_int, c_int]),
+    "ecgpu_galois_ilog": (c_int, [c_int, c_int]),
+    "ecgpu_reed_sol_vandermonde_coding_matrix": (c_void_p, [c_int, c_int, c_int]),
+    "ecgpu_reed_sol_extended_vandermonde_matrix": (c_void_p, [c_int, c_int, c_int]),
+    "ecgpu_reed_sol_big_vandermonde_distribution_matrix": (c_void_p, [c_int, c_int, c_int]),
+    "ecgpu_reed_sol_r6_coding_matrix": (c_void_p, [c_int, c_int]),
+    "ecgpu_jerasure_invert_matrix": (c_int, [c_int_p, c_int_p, c_int, c_int]),
+    "ecgpu_jerasure_invertible_matrix": (c_int, [c_int_p, c_int, c_int]),
+    "ecgpu_jerasure_matrix_multiply": (c_void_p, [c_int_p, c_int_p, c_int, c_int, c_int, c_int, c_int]),
+    "ecgpu_jerasure_erasures_to_erased": (c_void_p, [c_int, c_int, c_int_p]),
+    "ecgpu_jerasure_make_decoding_matrix": (c_int, [c_int, c_int, c_int, c_int_p, c_int_p, c_int_p, c_int_p]),
+    "ecgpu_decode_plan": (c_int, [c_int, c_int, c_int, c_int_p, c_int, c_int_p, c_int_p, c_int_p, c_int_p,
+                                  c_int_p, c_int_p]),
+    "ecgpu_jerasure_matrix_encode": (c_int, [c_int, c_int, c_int, c_int_p, c_void_pp, c_void_pp, c_int]),
+    "ecgpu_jerasure_matrix_decode": (c_int, [c_int, c_int, c_int, c_int_p, c_int, c_int_p, c_void_pp, c_void_pp,
+                                             c_int]),
+    "ecgpu_jerasure_matrix_dotprod": (c_int, [c_int, c_int, c_int_p, c_int_p, c_int, c_void_pp, c_void_pp, c_int]),
+    "ecgpu_jerasure_do_parity": (c_int, [c_int, c_void_pp, c_void_p, c_int]),
+    "ecgpu_galois_w08_region_multiply": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int]),
+    "ecgpu_galois_region_xor": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+    "ecgpu_reed_sol_r6_encode": (c_int, [c_int, c_int, c_void_pp, c_void_pp, c_int]),
+    "ecgpu_reed_sol_galois_w08_region_multby_2": (c_int, [c_void_p, c_int]),
+    "ecgpu_jerasure_get_stats": (c_int, [c_double_p]),
+    "ecgpu_plan_create": (c_void_p, [c_int, c_int, c_int_p, c_int]),
+    "ecgpu_plan_bind": (c_int, [c_void_p, c_int, c_void_pp, c_void_pp, c_int64]),
+    "ecgpu_plan_set_kernel": (c_int, [c_void_p, c_int, c_int]),
+    "ecgpu_plan_launch": (c_int, [c_void_p, c_void_p]),
+    "ecgpu_plan_destroy": (None, [c_void_p]),
+    "ecgpu_encode_batch": (c_int, [c_int, c_int, c_int_p, c_int, c_void_pp, c_void_pp, c_int64, c_void_p]),
+}
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _f = getattr(lib, _name)
+    _f.restype, _f.argtypes = _res, _args
+
+
+class EcgpuError(RuntimeError):
+    pass
+
+
+def last_error() -> str:
+    msg = lib.ecgpu_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> int:
+    if rc < ECGPU_ERR:  # ECGPU_ERR (-1) is a reference-style result, not an exception
+        raise EcgpuError(f"{what} failed ({rc}): {last_error()}")
+    return rc
+
+
+def int_array(values) -> ctypes.Array:
+    vals = [int(v) for v in values]
+    arr = (c_int * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = v
+    return arr
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    ptrs = list(ptrs)
+    arr = (c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr
+
+
+def take_int_matrix(addr: int, n: int) -> list:
+    """Copy n ints out of a malloc'd C array and free it (NULL -> None)."""
+    if not addr:
+        return None
+    out = list((c_int * n).from_address(addr))
+    lib.ecgpu_free(addr)
+    return out

@@ -1,0 +1,74 @@
+// capi_host.cpp -- host-only entry points of include/ecgpu.h (no GPU touched).
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "ecgpu.h"
+#include "gf_host.hpp"
+#include "matrix_host.hpp"
+#include "planner.hpp"
+
+using namespace ecgpu;
+
+extern "C" {
+
+ECGPU_API const char* ecgpu_version(void) { return "ecgpu 0.1 (gfx950)"; }
+ECGPU_API void ecgpu_free(void* p) { std::free(p); }
+
+ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w) { return single_multiply(a, b, w); }
+ECGPU_API int ecgpu_galois_single_divide(int a, int b, int w) { return single_divide(a, b, w); }
+ECGPU_API int ecgpu_galois_inverse(int a, int w) { return inverse(a, w); }
+ECGPU_API int ecgpu_galois_log(int value, int w) {
+  int* t = log_table(w);
+  return t ? t[value] : -1;
+}
+ECGPU_API int ecgpu_galois_ilog(int value, int w) {
+  int* t = ilog_table(w);
+  return t ? t[value] : -1;
+}
+
+ECGPU_API int* ecgpu_reed_sol_vandermonde_coding_matrix(int k, int m, int w) {
+  return vandermonde_coding_matrix(k, m, w);
+}
+ECGPU_API int* ecgpu_reed_sol_extended_vandermonde_matrix(int rows, int cols, int w) {
+  return extended_vandermonde_matrix(rows, cols, w);
+}
+ECGPU_API int* ecgpu_reed_sol_big_vandermonde_distribution_matrix(int rows, int cols, int w) {
+  return big_vandermonde_distribution_matrix(rows, cols, w);
+}
+ECGPU_API int* ecgpu_reed_sol_r6_coding_matrix(int k, int w) { return r6_coding_matrix(k, w); }
+ECGPU_API int ecgpu_jerasure_invert_matrix(int* mat, int* inv, int rows, int w) {
+  return invert_matrix(mat, inv, rows, w);
+}
+ECGPU_API int ecgpu_jerasure_invertible_matrix(int* mat, int rows, int w) { return invertible_matrix(mat, rows, w); }
+ECGPU_API int* ecgpu_jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, int r2, int c2, int w) {
+  return matrix_multiply(m1, m2, r1, c1, r2, c2, w);
+}
+ECGPU_API int* ecgpu_jerasure_erasures_to_erased(int k, int m, int* erasures) {
+  return erasures_to_erased(k, m, erasures);
+}
+ECGPU_API int ecgpu_jerasure_make_decoding_matrix(int k, int m, int w, int* matrix, int* erased, int* dm,
+                                                  int* dm_ids) {
+  return make_decoding_matrix(k, m, w, matrix, erased, dm, dm_ids);
+}
+
+// Replays the decode on symbolic buffers whose "pointers" are shard ids + 1,
+// then reads the fused map back in terms of ids.
+ECGPU_API int ecgpu_decode_plan(int k, int m, int w, const int* matrix, int row_k_ones, const int* erasures,
+                                int* out_ids, int* n_out, int* src_ids, int* n_src, int* coefs) {
+  if (w != 8 || k <= 0 || m <= 0 || !matrix || !erasures) return ECGPU_ERR_ARG;
+  std::vector<char*> ids(size_t(k + m));
+  for (int i = 0; i < k + m; ++i) ids[i] = reinterpret_cast<char*>(uintptr_t(i) + 1);
+  LinearTracker t;
+  for (int i = 0; i < k + m; ++i) t.id(ids[i]);
+  if (plan_decode(t, k, m, matrix, row_k_ones, erasures, ids.data(), ids.data() + k, 1) < 0) return ECGPU_ERR;
+  const FusedOp op = t.finish();
+  *n_out = int(op.dsts.size());
+  *n_src = int(op.srcs.size());
+  for (size_t r = 0; r < op.dsts.size(); ++r) out_ids[r] = int(reinterpret_cast<uintptr_t>(op.dsts[r]) - 1);
+  for (size_t j = 0; j < op.srcs.size(); ++j) src_ids[j] = int(reinterpret_cast<uintptr_t>(op.srcs[j]) - 1);
+  for (size_t i = 0; i < op.coef.size(); ++i) coefs[i] = op.coef[i];
+  return ECGPU_OK;
+}
+
+}  // extern "C"

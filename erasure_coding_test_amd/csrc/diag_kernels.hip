@@ -1,0 +1,72 @@
+// diag_kernels.hip -- TUNING/DIAGNOSTIC library (libecgpu_diag.so), not the
+// product.  Instantiates variants of the production kernel (gf_kernels.hpp)
+// so they can be A/B-timed in one process on the MI355X:
+//   variant 0: gf_apply_perm<K, R, VEC, MODE> for (K,R) in {(10,4), (10,1)},
+//              VEC in {1, 2, 4}, MODE in {table, mask, all-perm, xor-only}
+//   variant 1: diag_copy<VEC> -- 1 read + 1 write stream, the HBM reference
+//   variant 2: gf_apply_lds<K, R> (north-star LDS nibble tables)
+#include <hip/hip_runtime.h>
+
+#include "gf_kernels.hpp"
+
+using ecgpu::dev::ApplyArgs;
+using KernelFn = void (*)(ApplyArgs);
+
+namespace {
+template <int K, int R, int V>
+KernelFn pick_mode(int mode) {
+  switch (mode) {
+    case 0: return &ecgpu::dev::gf_apply_perm<K, R, V, 0>;
+    case 1: return &ecgpu::dev::gf_apply_perm<K, R, V, 1>;
+    case 2: return &ecgpu::dev::gf_apply_perm<K, R, V, 2>;
+    default: return &ecgpu::dev::gf_apply_perm<K, R, V, 3>;
+  }
+}
+template <int K, int R>
+KernelFn pick_vec(int vec, int mode) {
+  switch (vec) {
+    case 1: return pick_mode<K, R, 1>(mode);
+    case 2: return pick_mode<K, R, 2>(mode);
+    default: return pick_mode<K, R, 4>(mode);
+  }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
+    int variant, int K, int R, int vec, int mode, const void* qtab, const void* ntab, const void* src_tab,
+    void* dst_tab, int stripes, long long size, unsigned long long unit_mask, unsigned long long zero_mask, int nt,
+    void* stream) {
+  KernelFn fn = nullptr;
+  if (variant == 0) {
+    if (K == 10 && R == 4) fn = pick_vec<10, 4>(vec, mode);
+    if (K == 10 && R == 1) fn = pick_vec<10, 1>(vec, mode);
+  } else if (variant == 1) {
+    fn = vec == 1 ? &ecgpu::dev::diag_copy<1> : vec == 2 ? &ecgpu::dev::diag_copy<2> : &ecgpu::dev::diag_copy<4>;
+  } else if (variant == 2) {
+    vec = 1;
+    if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_lds<10, 4>;
+    if (K == 10 && R == 1) fn = &ecgpu::dev::gf_apply_lds<10, 1>;
+  }
+  if (!fn) return -2;
+  ApplyArgs a{};
+  a.qtab = static_cast<const ecgpu::dev::u32x4*>(qtab);
+  a.ntab = static_cast<const uint8_t*>(ntab);
+  a.src = static_cast<const uint8_t* const*>(src_tab);
+  a.dst = static_cast<uint8_t* const*>(dst_tab);
+  a.nvec = size / 16;
+  a.size = size;
+  a.byte0 = a.nvec * 16;
+  a.unit_mask = unit_mask;
+  a.zero_mask = zero_mask;
+  a.src_stride = variant == 1 ? 1 : K;
+  a.dst_stride = variant == 1 ? 1 : R;
+  a.row0 = 0;
+  a.K = K;
+  a.R = R;
+  a.nt = nt;
+  const long long per_block = 256LL * vec;
+  dim3 grid(unsigned((a.nvec + per_block - 1) / per_block), unsigned(stripes));
+  void* args[] = {&a};
+  return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(256), args, 0,
+                         static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -3;
+}

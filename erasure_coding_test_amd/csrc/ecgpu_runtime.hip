@@ -1,0 +1,609 @@
+// ecgpu_runtime.hip -- device side of include/ecgpu.h: plans, kernel
+// dispatch, staging of host buffers, and the hot-path C ABI.
+//
+// Execution model (MI355X-first, not the reference's byte loops):
+//   * every hot-path call is planned on the host into ONE fused
+//     rows x nsrc GF(2^8) matrix apply (planner.hpp) and runs as one
+//     streaming launch per <= 4 output rows;
+//   * buffers are classified per pointer: device memory is used in place,
+//     host memory is staged through a per-context HBM slab with
+//     hipMemcpyAsync on that context's own non-blocking stream;
+//   * contexts (stream + staging + plan cache) come from a process-wide
+//     pool, so concurrent callers (the reference's encode pthreads,
+//     client_main.cpp:1074-1164) never share a stream or a lock on the
+//     submit path; tables are built once (std::call_once in gf_host).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <list>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "ecgpu.h"
+#include "gf_host.hpp"
+#include "gf_kernels.hpp"
+#include "matrix_host.hpp"
+#include "planner.hpp"
+
+using namespace ecgpu;
+using dev::ApplyArgs;
+using dev::u32x4;
+
+namespace {
+
+thread_local std::string t_err;
+
+int fail(int code, const std::string& msg) {
+  t_err = msg;
+  return code;
+}
+
+#define ECGPU_HIP(expr)                                                                          \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      return fail(ECGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// ------------------------------------------------------- kernel tables ----
+using KernelFn = void (*)(ApplyArgs);
+
+// Production kernel shape (chosen by A/B on MI355X):
+// one 16-B column per lane, 0/1 coefficients classified by kernarg masks.
+constexpr int kProdVec = 1;
+constexpr int kProdMode = dev::kClassFromMask;
+
+template <int K, int R>
+constexpr KernelFn perm_fn() { return &dev::gf_apply_perm<K, R, kProdVec, kProdMode>; }
+template <int K, int R>
+constexpr KernelFn lds_fn() { return &dev::gf_apply_lds<K, R>; }
+
+template <int K>
+struct Row {
+  static constexpr KernelFn perm[4] = {perm_fn<K, 1>(), perm_fn<K, 2>(), perm_fn<K, 3>(), perm_fn<K, 4>()};
+  static constexpr KernelFn lds[4] = {lds_fn<K, 1>(), lds_fn<K, 2>(), lds_fn<K, 3>(), lds_fn<K, 4>()};
+};
+
+template <int... Ks>
+struct Table {
+  static KernelFn get(bool lds, int K, int R) {
+    KernelFn out = nullptr;
+    ((K == Ks ? (out = lds ? Row<Ks>::lds[R - 1] : Row<Ks>::perm[R - 1], 0) : 0), ...);
+    return out;
+  }
+};
+using SpecTable = Table<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
+
+KernelFn generic_fn(int R) {
+  switch (R) {
+    case 1: return &dev::gf_apply_perm_generic<1>;
+    case 2: return &dev::gf_apply_perm_generic<2>;
+    case 3: return &dev::gf_apply_perm_generic<3>;
+    default: return &dev::gf_apply_perm_generic<4>;
+  }
+}
+
+hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t s) {
+  void* args[] = {&a};
+  return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, block, args, 0, s);
+}
+
+// Per-coefficient tables.  PERM: word p holds c*(e << 2p) in byte e.  LDS:
+// 16 low-nibble products then 16 high-nibble products.
+void build_tables(int c, u32x4* q, uint8_t* nib) {
+  const auto& T = gf8().mul[c & 0xFF];
+  uint32_t w[4];
+  for (int p = 0; p < 4; ++p) {
+    w[p] = 0;
+    for (int e = 0; e < 4; ++e) w[p] |= uint32_t(T[e << (2 * p)]) << (8 * e);
+  }
+  *q = u32x4{w[0], w[1], w[2], w[3]};
+  for (int x = 0; x < 16; ++x) {
+    nib[x] = T[x];
+    nib[16 + x] = T[x << 4];
+  }
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------- plan ----
+struct ecgpu_plan {
+  int device = 0, rows = 0, nsrc = 0;
+  int kind = ECGPU_KERNEL_PERM, nt = 1;
+  std::vector<uint8_t> coef;  // host copy, rows x nsrc
+  u32x4* d_q = nullptr;
+  uint8_t* d_nib = nullptr;
+  int stripes = 0;
+  int64_t size = 0;
+  bool aligned = true;
+  const uint8_t** d_src = nullptr;
+  uint8_t** d_dst = nullptr;
+  size_t cap_src = 0, cap_dst = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+void plan_free(ecgpu_plan* p) {
+  if (!p) return;
+  DeviceGuard g(p->device);
+  if (p->d_q) (void)hipFree(p->d_q);
+  if (p->d_nib) (void)hipFree(p->d_nib);
+  if (p->d_src) (void)hipFree(p->d_src);
+  if (p->d_dst) (void)hipFree(p->d_dst);
+  delete p;
+}
+
+int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device) {
+  p->device = device;
+  p->rows = rows;
+  p->nsrc = nsrc;
+  p->kind = env_int("ECGPU_KERNEL", ECGPU_KERNEL_PERM);
+  p->nt = env_int("ECGPU_NT", 1);
+  const size_t n = size_t(rows) * nsrc;
+  p->coef.resize(n);
+  for (size_t i = 0; i < n; ++i) p->coef[i] = uint8_t(coefs[i] & 0xFF);
+  std::vector<u32x4> q(n);
+  std::vector<uint8_t> nib(n * 32);
+  for (size_t i = 0; i < n; ++i) build_tables(coefs[i], &q[i], &nib[i * 32]);
+  DeviceGuard g(device);
+  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_q), n * sizeof(u32x4)));
+  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_nib), n * 32));
+  ECGPU_HIP(hipMemcpy(p->d_q, q.data(), n * sizeof(u32x4), hipMemcpyHostToDevice));
+  ECGPU_HIP(hipMemcpy(p->d_nib, nib.data(), n * 32, hipMemcpyHostToDevice));
+  return ECGPU_OK;
+}
+
+int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* const* dst, int64_t size,
+              hipStream_t stream) {
+  const size_t ns = size_t(stripes) * p->nsrc, nd = size_t(stripes) * p->rows;
+  DeviceGuard g(p->device);
+  if (ns > p->cap_src) {
+    if (p->d_src) ECGPU_HIP(hipFree(p->d_src));
+    p->d_src = nullptr;
+    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_src), ns * sizeof(void*)));
+    p->cap_src = ns;
+  }
+  if (nd > p->cap_dst) {
+    if (p->d_dst) ECGPU_HIP(hipFree(p->d_dst));
+    p->d_dst = nullptr;
+    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_dst), nd * sizeof(void*)));
+    p->cap_dst = nd;
+  }
+  bool aligned = true;
+  for (size_t i = 0; i < ns; ++i) aligned &= (reinterpret_cast<uintptr_t>(src[i]) & 15u) == 0;
+  for (size_t i = 0; i < nd; ++i) aligned &= (reinterpret_cast<uintptr_t>(dst[i]) & 15u) == 0;
+  if (stream) {
+    ECGPU_HIP(hipMemcpyAsync(p->d_src, src, ns * sizeof(void*), hipMemcpyHostToDevice, stream));
+    ECGPU_HIP(hipMemcpyAsync(p->d_dst, dst, nd * sizeof(void*), hipMemcpyHostToDevice, stream));
+    ECGPU_HIP(hipStreamSynchronize(stream));  // host tables may die after return
+  } else {
+    ECGPU_HIP(hipMemcpy(p->d_src, src, ns * sizeof(void*), hipMemcpyHostToDevice));
+    ECGPU_HIP(hipMemcpy(p->d_dst, dst, nd * sizeof(void*), hipMemcpyHostToDevice));
+  }
+  p->stripes = stripes;
+  p->size = size;
+  p->aligned = aligned;
+  return ECGPU_OK;
+}
+
+int plan_launch(ecgpu_plan* p, hipStream_t stream) {
+  if (p->stripes <= 0 || p->size <= 0 || p->rows <= 0) return ECGPU_OK;
+  DeviceGuard g(p->device);
+  const int K = p->nsrc;
+  const int64_t nvec = p->aligned ? p->size / 16 : 0;
+  const int64_t byte0 = nvec * 16;
+  const dim3 block(dev::kBlock);
+  constexpr int kMaxGridY = 65535;
+  for (int r0 = 0; r0 < p->rows; r0 += dev::kMaxRows) {
+    const int R = std::min(dev::kMaxRows, p->rows - r0);
+    const bool spec = K <= dev::kMaxSpecK;
+    KernelFn vec_fn = spec ? SpecTable::get(p->kind == ECGPU_KERNEL_LDS, K, R) : generic_fn(R);
+    const int vec = (spec && p->kind != ECGPU_KERNEL_LDS) ? kProdVec : 1;
+    uint64_t unit = 0, zero = 0;
+    if (spec)
+      for (int r = 0; r < R; ++r)
+        for (int j = 0; j < K; ++j) {
+          const uint8_t c = p->coef[size_t(r0 + r) * K + j];
+          if (c == 1) unit |= uint64_t(1) << (r * K + j);
+          if (c == 0) zero |= uint64_t(1) << (r * K + j);
+        }
+    for (int s0 = 0; s0 < p->stripes; s0 += kMaxGridY) {
+      const int ns = std::min(kMaxGridY, p->stripes - s0);
+      ApplyArgs a{};
+      a.qtab = p->d_q + size_t(r0) * K;
+      a.ntab = p->d_nib + size_t(r0) * K * 32;
+      a.src = p->d_src + size_t(s0) * K;
+      a.dst = p->d_dst + size_t(s0) * p->rows;
+      a.nvec = nvec;
+      a.size = p->size;
+      a.byte0 = byte0;
+      a.src_stride = K;
+      a.dst_stride = p->rows;
+      a.row0 = r0;
+      a.K = K;
+      a.R = R;
+      a.nt = p->nt;
+      a.unit_mask = unit;
+      a.zero_mask = zero;
+      if (nvec > 0) {
+        const int64_t per_block = int64_t(dev::kBlock) * vec;
+        const dim3 grid(unsigned((nvec + per_block - 1) / per_block), unsigned(ns));
+        ECGPU_HIP(launch(vec_fn, grid, block, a, stream));
+      }
+      if (byte0 < p->size) {
+        const dim3 grid(unsigned((p->size - byte0 + dev::kBlock - 1) / dev::kBlock), unsigned(ns));
+        ECGPU_HIP(launch(&dev::gf_apply_bytes, grid, block, a, stream));
+      }
+    }
+  }
+  return ECGPU_OK;
+}
+
+// ------------------------------------------------------ context pool ----
+struct PlanKey {
+  int rows, nsrc;
+  std::vector<uint8_t> coef;
+  bool operator==(const PlanKey& o) const { return rows == o.rows && nsrc == o.nsrc && coef == o.coef; }
+};
+
+struct Ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* stage = nullptr;
+  size_t stage_cap = 0;
+  std::list<std::pair<PlanKey, ecgpu_plan*>> plans;  // LRU, front = newest
+};
+
+std::mutex g_pool_mu;
+std::vector<Ctx*> g_pool;  // idle contexts; never destroyed (process lifetime)
+
+int current_device() {
+  const int forced = env_int("ECGPU_DEVICE", -1);
+  if (forced >= 0) return forced;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) d = 0;
+  return d;
+}
+
+Ctx* acquire_ctx(int device, int* rc) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size(); ++i)
+      if (g_pool[i]->device == device) {
+        Ctx* c = g_pool[i];
+        g_pool.erase(g_pool.begin() + long(i));
+        *rc = ECGPU_OK;
+        return c;
+      }
+  }
+  auto* c = new Ctx();
+  c->device = device;
+  DeviceGuard g(device);
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    *rc = fail(ECGPU_ERR_HIP, std::string("hipStreamCreateWithFlags: ") + hipGetErrorString(e));
+    delete c;
+    return nullptr;
+  }
+  *rc = ECGPU_OK;
+  return c;
+}
+
+void release_ctx(Ctx* c) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool.push_back(c);
+}
+
+struct CtxLease {
+  Ctx* c = nullptr;
+  int rc = ECGPU_OK;
+  explicit CtxLease(int device) : c(acquire_ctx(device, &rc)) {}
+  ~CtxLease() {
+    if (c) release_ctx(c);
+  }
+};
+
+int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint8_t>& coef, ecgpu_plan** out) {
+  PlanKey key{rows, nsrc, coef};
+  for (auto it = c->plans.begin(); it != c->plans.end(); ++it)
+    if (it->first == key) {
+      c->plans.splice(c->plans.begin(), c->plans, it);
+      *out = it->second;
+      return ECGPU_OK;
+    }
+  auto* p = new ecgpu_plan();
+  std::vector<int> ci(coef.begin(), coef.end());
+  int rc = plan_init(p, rows, nsrc, ci.data(), c->device);
+  if (rc != ECGPU_OK) {
+    plan_free(p);
+    return rc;
+  }
+  c->plans.emplace_front(std::move(key), p);
+  if (c->plans.size() > 64) {
+    plan_free(c->plans.back().second);
+    c->plans.pop_back();
+  }
+  *out = p;
+  return ECGPU_OK;
+}
+
+int ensure_stage(Ctx* c, size_t bytes) {
+  if (bytes <= c->stage_cap) return ECGPU_OK;
+  DeviceGuard g(c->device);
+  if (c->stage) ECGPU_HIP(hipFree(c->stage));
+  c->stage = nullptr;
+  c->stage_cap = 0;
+  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&c->stage), bytes));
+  c->stage_cap = bytes;
+  return ECGPU_OK;
+}
+
+// Is p device memory of `device` (usable in place)?  Host memory (pageable or
+// pinned) is staged; device memory of another GPU is rejected.
+int classify(const void* p, int device, bool* on_device) {
+  hipPointerAttribute_t attr;
+  hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *on_device = false;
+    return ECGPU_OK;
+  }
+  if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) {
+    if (attr.device != device)
+      return fail(ECGPU_ERR_ARG, "buffer lives on device " + std::to_string(attr.device) + ", call runs on " +
+                                     std::to_string(device));
+    *on_device = true;
+    return ECGPU_OK;
+  }
+  *on_device = false;
+  return ECGPU_OK;
+}
+
+// ------------------------------------------------------ stats counters ----
+std::mutex g_stats_mu;
+double g_stats[3] = {0, 0, 0};  // xor, gf, memcpy -- jerasure.cpp:1145-1147 order
+
+void add_stats(const FusedOp& op) {
+  std::lock_guard<std::mutex> lk(g_stats_mu);
+  g_stats[0] += op.xor_bytes;
+  g_stats[1] += op.gf_bytes;
+  g_stats[2] += op.memcpy_bytes;
+}
+
+// Runs a fused op synchronously over `size` bytes of every buffer.
+int execute(const FusedOp& op, int64_t size) {
+  add_stats(op);
+  if (op.dsts.empty() || size <= 0) return ECGPU_OK;
+  const int device = current_device();
+  CtxLease lease(device);
+  if (!lease.c) return lease.rc;
+  Ctx* c = lease.c;
+  DeviceGuard g(device);
+
+  // Map every distinct buffer to a device address (in place or a staging slot).
+  std::vector<void*> bufs = op.srcs;
+  for (void* d : op.dsts)
+    if (std::find(bufs.begin(), bufs.end(), d) == bufs.end()) bufs.push_back(d);
+  const size_t slot = (size_t(size) + 255) & ~size_t(255);
+  std::vector<uint8_t*> devp(bufs.size(), nullptr);
+  std::vector<char> staged(bufs.size(), 0);
+  size_t nstage = 0;
+  for (size_t i = 0; i < bufs.size(); ++i) {
+    bool on_dev = false;
+    int rc = classify(bufs[i], device, &on_dev);
+    if (rc != ECGPU_OK) return rc;
+    if (on_dev) {
+      devp[i] = static_cast<uint8_t*>(bufs[i]);
+    } else {
+      staged[i] = 1;
+      ++nstage;
+    }
+  }
+  const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
+  // With several launches (> 4 rows) an output that is also a source must
+  // not be overwritten before the last launch reads it: write to temps.
+  const bool via_temp = op.dst_is_src && rows > dev::kMaxRows;
+  const size_t ntemp = via_temp ? size_t(rows) : 0;
+  int rc = ensure_stage(c, (nstage + ntemp) * slot);
+  if (rc != ECGPU_OK) return rc;
+  size_t next = 0;
+  for (size_t i = 0; i < bufs.size(); ++i)
+    if (staged[i]) devp[i] = c->stage + (next++) * slot;
+  for (size_t j = 0; j < op.srcs.size(); ++j)
+    if (staged[j])
+      ECGPU_HIP(hipMemcpyAsync(devp[j], op.srcs[j], size_t(size), hipMemcpyHostToDevice, c->stream));
+
+  std::vector<const uint8_t*> sp(static_cast<size_t>(nsrc));
+  std::vector<uint8_t*> dp(static_cast<size_t>(rows));
+  for (int j = 0; j < nsrc; ++j) sp[j] = devp[j];
+  for (int r = 0; r < rows; ++r) {
+    const size_t i = size_t(std::find(bufs.begin(), bufs.end(), op.dsts[r]) - bufs.begin());
+    dp[r] = via_temp ? c->stage + (nstage + size_t(r)) * slot : devp[i];
+  }
+  if (nsrc == 0) {
+    // Every output is identically zero (e.g. region multiply by 0 without
+    // add, galois.cpp:447-451): nothing to read.
+    for (int r = 0; r < rows; ++r) ECGPU_HIP(hipMemsetAsync(dp[r], 0, size_t(size), c->stream));
+  } else {
+    ecgpu_plan* p = nullptr;
+    rc = ctx_plan(c, rows, nsrc, op.coef, &p);
+    if (rc != ECGPU_OK) return rc;
+    rc = plan_bind(p, 1, sp.data(), dp.data(), size, c->stream);
+    if (rc != ECGPU_OK) return rc;
+    rc = plan_launch(p, c->stream);
+    if (rc != ECGPU_OK) return rc;
+  }
+  for (int r = 0; r < rows; ++r) {
+    const size_t i = size_t(std::find(bufs.begin(), bufs.end(), op.dsts[r]) - bufs.begin());
+    if (via_temp)
+      ECGPU_HIP(hipMemcpyAsync(devp[i], dp[r], size_t(size), hipMemcpyDeviceToDevice, c->stream));
+    if (staged[i])
+      ECGPU_HIP(hipMemcpyAsync(op.dsts[r], devp[i], size_t(size), hipMemcpyDeviceToHost, c->stream));
+  }
+  ECGPU_HIP(hipStreamSynchronize(c->stream));
+  ECGPU_HIP(hipGetLastError());
+  return ECGPU_OK;
+}
+
+}  // namespace
+
+// ================================================================ C ABI ====
+extern "C" {
+
+ECGPU_API const char* ecgpu_last_error(void) { return t_err.c_str(); }
+
+ECGPU_API ecgpu_plan* ecgpu_plan_create(int rows, int nsrc, const int* coefs, int device) {
+  if (rows <= 0 || nsrc <= 0 || !coefs) {
+    fail(ECGPU_ERR_ARG, "ecgpu_plan_create: rows, nsrc > 0 and coefs required");
+    return nullptr;
+  }
+  if (device < 0) device = current_device();
+  auto* p = new ecgpu_plan();
+  if (plan_init(p, rows, nsrc, coefs, device) != ECGPU_OK) {
+    plan_free(p);
+    return nullptr;
+  }
+  return p;
+}
+
+ECGPU_API int ecgpu_plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src_ptrs, uint8_t* const* dst_ptrs,
+                              int64_t size) {
+  if (!p || stripes < 0 || size < 0 || (stripes && (!src_ptrs || !dst_ptrs)))
+    return fail(ECGPU_ERR_ARG, "ecgpu_plan_bind: bad arguments");
+  return plan_bind(p, stripes, src_ptrs, dst_ptrs, size, nullptr);
+}
+
+ECGPU_API int ecgpu_plan_set_kernel(ecgpu_plan* p, int kind, int nontemporal) {
+  if (!p || (kind != ECGPU_KERNEL_PERM && kind != ECGPU_KERNEL_LDS))
+    return fail(ECGPU_ERR_ARG, "ecgpu_plan_set_kernel: bad arguments");
+  p->kind = kind;
+  p->nt = nontemporal ? 1 : 0;
+  return ECGPU_OK;
+}
+
+ECGPU_API int ecgpu_plan_launch(ecgpu_plan* p, void* stream) {
+  if (!p) return fail(ECGPU_ERR_ARG, "ecgpu_plan_launch: null plan");
+  return plan_launch(p, static_cast<hipStream_t>(stream));
+}
+
+ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p) { plan_free(p); }
+
+ECGPU_API int ecgpu_encode_batch(int k, int m, const int* matrix, int stripes, const uint8_t* const* data,
+                                 uint8_t* const* coding, int64_t size, void* stream) {
+  if (k <= 0 || m <= 0 || !matrix) return fail(ECGPU_ERR_ARG, "ecgpu_encode_batch: bad arguments");
+  ecgpu_plan* p = ecgpu_plan_create(m, k, matrix, -1);
+  if (!p) return ECGPU_ERR_HIP;
+  int rc = plan_bind(p, stripes, data, coding, size, static_cast<hipStream_t>(stream));
+  if (rc == ECGPU_OK) rc = plan_launch(p, static_cast<hipStream_t>(stream));
+  if (rc == ECGPU_OK && stream) {
+    hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) rc = fail(ECGPU_ERR_HIP, hipGetErrorString(e));
+  } else if (rc == ECGPU_OK) {
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) rc = fail(ECGPU_ERR_HIP, hipGetErrorString(e));
+  }
+  plan_free(p);
+  return rc;
+}
+
+ECGPU_API int ecgpu_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs,
+                                           int size) {
+  if (w != 8) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_encode: w must be 8");
+  LinearTracker t;
+  plan_encode(t, k, m, matrix, data_ptrs, coding_ptrs, size);
+  return execute(t.finish(), size);
+}
+
+ECGPU_API int ecgpu_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures,
+                                           char** data_ptrs, char** coding_ptrs, int size) {
+  if (w != 8) return w == 16 || w == 32 ? fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_decode: w must be 8") : -1;
+  LinearTracker t;
+  if (plan_decode(t, k, m, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size) < 0) return ECGPU_ERR;
+  return execute(t.finish(), size);
+}
+
+ECGPU_API int ecgpu_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int dest_id,
+                                            char** data_ptrs, char** coding_ptrs, int size) {
+  if (w != 8) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_dotprod: w must be 8");
+  LinearTracker t;
+  t.dotprod(k, matrix_row, src_ids, dest_id, data_ptrs, coding_ptrs, size);
+  return execute(t.finish(), size);
+}
+
+ECGPU_API int ecgpu_jerasure_do_parity(int k, char** data_ptrs, char* parity_ptr, int size) {
+  LinearTracker t;
+  t.copy(parity_ptr, data_ptrs[0]);
+  for (int i = 1; i < k; ++i) t.xor3(data_ptrs[i], parity_ptr, parity_ptr);
+  t.count(double(size) * (k - 1), 0, double(size));
+  return execute(t.finish(), size);
+}
+
+ECGPU_API int ecgpu_galois_w08_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
+  LinearTracker t;
+  if (r2 == nullptr)
+    t.mul(region, multby, region, false);  // galois.cpp:429,447: in place, add ignored
+  else
+    t.mul(region, multby, r2, add != 0);
+  return execute(t.finish(), nbytes);
+}
+
+ECGPU_API int ecgpu_galois_region_xor(char* r1, char* r2, char* r3, int nbytes) {
+  LinearTracker t;
+  t.xor3(r1, r2, r3);
+  return execute(t.finish(), nbytes);
+}
+
+ECGPU_API int ecgpu_reed_sol_galois_w08_region_multby_2(char* region, int nbytes) {
+  LinearTracker t;
+  t.mul(region, 2, region, false);
+  return execute(t.finish(), nbytes);
+}
+
+// reed_sol.cpp:200-225 (w = 8): P = XOR of data; Q = Horner sum of 2^j d_j.
+ECGPU_API int ecgpu_reed_sol_r6_encode(int k, int w, char** data_ptrs, char** coding_ptrs, int size) {
+  if (w != 8) return fail(ECGPU_ERR_ARG, "ecgpu_reed_sol_r6_encode: w must be 8");
+  LinearTracker t;
+  t.copy(coding_ptrs[0], data_ptrs[0]);
+  for (int i = 1; i < k; ++i) t.xor3(coding_ptrs[0], data_ptrs[i], coding_ptrs[0]);
+  t.copy(coding_ptrs[1], data_ptrs[k - 1]);
+  for (int i = k - 2; i >= 0; --i) {
+    t.mul(coding_ptrs[1], 2, coding_ptrs[1], false);
+    t.xor3(coding_ptrs[1], data_ptrs[i], coding_ptrs[1]);
+  }
+  const int rc = execute(t.finish(), size);
+  return rc == ECGPU_OK ? 1 : rc;
+}
+
+ECGPU_API int ecgpu_jerasure_get_stats(double* fill_in) {
+  std::lock_guard<std::mutex> lk(g_stats_mu);
+  for (int i = 0; i < 3; ++i) {
+    fill_in[i] = g_stats[i];
+    g_stats[i] = 0;
+  }
+  return ECGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,322 @@
+// gf_kernels.hpp -- CDNA4 (gfx950) kernels for the fused GF(2^8) matrix apply
+//
+//     dst[s][r][x] = XOR_j  coef[r][j] * src[s][j][x]      (GF(2^8), poly 0x11D)
+//
+// for every stripe s, output row r < R (<= 4 per launch) and byte x.  This
+// one primitive carries jerasure_matrix_encode, _decode, _dotprod and the
+// galois region ops (see planner.hpp).  It is HBM-bound integer byte work:
+// no MFMA; 16-byte coalesced loads/stores; all K source columns of a lane
+// are loaded before any arithmetic so a wave has K*16 B per lane in flight.
+//
+// Two multiply engines:
+//  * PERM (default): c*x is GF(2)-linear in x, so split every byte into four
+//    2-bit slices, c*x = T0[x&3] ^ T1[(x>>2)&3] ^ T2[(x>>4)&3] ^ T3[x>>6] with
+//    Tp[e] = c*(e << 2p).  Each Tp is 4 bytes = ONE dword, so one v_perm_b32
+//    looks up 4 bytes at once with the table held in a (scalar) register:
+//    4 v_perm + 2 v_xor3 per coefficient per dword, tables fetched by
+//    s_load (wave-uniform), no LDS, no bank conflicts.  The 4 selector words
+//    are computed once per source dword and shared by all R rows.
+//  * LDS (the north-star layout): per coefficient the two 16-entry nibble
+//    tables T_lo[x] = c*x, T_hi[x] = c*(x<<4) are staged once per workgroup
+//    in LDS (32 B per coefficient; a 16-B table spans 4 banks, so lanes of
+//    one group never conflict) and every byte costs 2 ds_read_u8.
+// Coefficients 0 and 1 are detected from the (uniform) table word and take a
+// scalar branch: skip / plain XOR.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ecgpu {
+namespace dev {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;              // 4 waves
+constexpr int kMaxRows = 4;              // rows per launch
+constexpr int kMaxSpecK = 16;            // K specialised at compile time
+constexpr uint32_t kQ0Unit = 0x03020100u;  // PERM table word 0 of coefficient 1
+constexpr uint32_t kLo2 = 0x03030303u;
+
+struct ApplyArgs {
+  const u32x4* qtab;              // [R][K] PERM tables (16 B each)
+  const uint8_t* ntab;            // [R][K][32] nibble tables (LDS engine)
+  const uint8_t* const* src;      // [stripes][src_stride] device pointers
+  uint8_t* const* dst;            // [stripes][dst_stride] device pointers
+  int64_t nvec;                   // 16-B columns per shard in the vector part
+  int64_t size;                   // bytes per shard
+  int64_t byte0;                  // first byte handled by the byte kernel
+  uint64_t unit_mask;             // bit r*K+j: coefficient == 1 (this launch's rows)
+  uint64_t zero_mask;             // bit r*K+j: coefficient == 0
+  int src_stride, dst_stride, row0;  // row0 = first dst column of this launch
+  int K, R;                       // runtime copies (generic / byte kernels)
+  int nt;                         // 1: non-temporal loads/stores
+};
+
+// How a launch treats coefficients 0 and 1.
+enum CoefMode : int {
+  kClassFromTable = 0,  // test the (s_load'ed) table word: 0 -> skip, unit -> XOR
+  kClassFromMask = 1,   // test kernarg bit masks (no load on the branch path)
+  kAllPerm = 2,         // no test: every coefficient through v_perm
+  kXorOnly = 3,         // DIAGNOSTIC: XOR all sources, ignore coefficients
+};
+
+__device__ __forceinline__ uint32_t perm_lookup(uint32_t table, uint32_t sel) {
+  // v_perm_b32: selector bytes 0..3 pick bytes of the second operand.
+  return __builtin_amdgcn_perm(table, table, sel);
+}
+
+__device__ __forceinline__ uint32_t gf_mul_perm(const u32x4& q, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) {
+  return perm_lookup(q.x, s0) ^ perm_lookup(q.y, s1) ^ perm_lookup(q.z, s2) ^ perm_lookup(q.w, s3);
+}
+
+__device__ __forceinline__ u32x4 load16(const uint8_t* p, int64_t col, int nt) {
+  const u32x4* a = reinterpret_cast<const u32x4*>(p) + col;
+  return nt ? __builtin_nontemporal_load(a) : *a;
+}
+
+__device__ __forceinline__ void store16(uint8_t* p, int64_t col, const u32x4& v, int nt) {
+  u32x4* a = reinterpret_cast<u32x4*>(p) + col;
+  if (nt)
+    __builtin_nontemporal_store(v, a);
+  else
+    *a = v;
+}
+
+// acc ^= c * v for one 16-byte column; sel = the four 2-bit selector words.
+template <int MODE>
+__device__ __forceinline__ void mac16(const ApplyArgs& a, int idx, const u32x4& v, const u32x4 (&sel)[4], u32x4& acc) {
+  if (MODE == kXorOnly) {
+    acc ^= v;
+    return;
+  }
+  if (MODE == kClassFromMask) {
+    if ((a.zero_mask >> idx) & 1u) return;
+    if ((a.unit_mask >> idx) & 1u) {
+      acc ^= v;
+      return;
+    }
+  }
+  const u32x4 q = a.qtab[idx];
+  if (MODE == kClassFromTable) {
+    if (q.x == 0u) return;      // coefficient 0
+    if (q.x == kQ0Unit) {       // coefficient 1
+      acc ^= v;
+      return;
+    }
+  }
+  acc.x ^= gf_mul_perm(q, sel[0].x, sel[1].x, sel[2].x, sel[3].x);
+  acc.y ^= gf_mul_perm(q, sel[0].y, sel[1].y, sel[2].y, sel[3].y);
+  acc.z ^= gf_mul_perm(q, sel[0].z, sel[1].z, sel[2].z, sel[3].z);
+  acc.w ^= gf_mul_perm(q, sel[0].w, sel[1].w, sel[2].w, sel[3].w);
+}
+
+// ---------------------------------------------------------------- PERM ----
+// Lane l of block b handles 16-byte columns b*VEC*256 + v*256 + l (v < VEC)
+// of every shard of stripe blockIdx.y: all K*VEC loads are issued before
+// any arithmetic, then R*VEC 16-byte stores.
+template <int K, int R, int VEC, int MODE>
+__global__ __launch_bounds__(kBlock) void gf_apply_perm(ApplyArgs a) {
+  const int64_t col0 = int64_t(blockIdx.x) * (VEC * kBlock) + threadIdx.x;
+  if (col0 >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+
+  bool live[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) live[v] = (col0 + v * kBlock) < a.nvec;
+
+  u32x4 x[VEC][K];
+  if (a.nt) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+#pragma unroll
+      for (int j = 0; j < K; ++j) x[v][j] = live[v] ? load16(sp[j], col0 + v * kBlock, 1) : u32x4{0u, 0u, 0u, 0u};
+  } else {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+#pragma unroll
+      for (int j = 0; j < K; ++j) x[v][j] = live[v] ? load16(sp[j], col0 + v * kBlock, 0) : u32x4{0u, 0u, 0u, 0u};
+  }
+
+  u32x4 acc[VEC][R];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v)
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[v][r] = u32x4{0u, 0u, 0u, 0u};
+
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      const u32x4 xv = x[v][j];
+      u32x4 sel[4];
+      if (MODE != kXorOnly) {
+        sel[0] = xv & kLo2;
+        sel[1] = (xv >> 2) & kLo2;
+        sel[2] = (xv >> 4) & kLo2;
+        sel[3] = (xv >> 6) & kLo2;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) mac16<MODE>(a, r * K + j, xv, sel, acc[v][r]);
+    }
+  }
+
+  if (a.nt) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+      if (live[v])
+#pragma unroll
+        for (int r = 0; r < R; ++r) store16(dp[r], col0 + v * kBlock, acc[v][r], 1);
+  } else {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+      if (live[v])
+#pragma unroll
+        for (int r = 0; r < R; ++r) store16(dp[r], col0 + v * kBlock, acc[v][r], 0);
+  }
+}
+
+// DIAGNOSTIC: streaming copy of shard 0 -> dst 0 (the HBM ceiling reference).
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void diag_copy(ApplyArgs a) {
+  const int64_t col0 = int64_t(blockIdx.x) * (VEC * kBlock) + threadIdx.x;
+  const int s = blockIdx.y;
+  const uint8_t* sp = a.src[int64_t(s) * a.src_stride];
+  uint8_t* dp = a.dst[int64_t(s) * a.dst_stride];
+  u32x4 x[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v)
+    if (col0 + v * kBlock < a.nvec) x[v] = load16(sp, col0 + v * kBlock, a.nt);
+#pragma unroll
+  for (int v = 0; v < VEC; ++v)
+    if (col0 + v * kBlock < a.nvec) store16(dp, col0 + v * kBlock, x[v], a.nt);
+}
+
+// ----------------------------------------------------------------- LDS ----
+__device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t* t, uint32_t lo, uint32_t hi) {
+  // lo/hi hold the low/high nibble of each byte in byte lanes 0..3.
+  uint32_t p = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const uint32_t e = uint32_t(t[(lo >> (8 * b)) & 0xFu]) ^ uint32_t(t[16 + ((hi >> (8 * b)) & 0xFu)]);
+    p |= e << (8 * b);
+  }
+  return p;
+}
+
+template <int K, int R>
+__global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lut[R * K * 32];
+  for (int i = threadIdx.x; i < R * K * 2; i += kBlock)
+    reinterpret_cast<u32x4*>(lut)[i] = reinterpret_cast<const u32x4*>(a.ntab)[i];
+  __syncthreads();
+
+  const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, a.nt);
+
+  u32x4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const u32x4 v = x[j];
+    const u32x4 lo = v & 0x0F0F0F0Fu, hi = (v >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t q0 = a.qtab[r * K + j].x;
+      if (q0 == 0u) continue;
+      if (q0 == kQ0Unit) {
+        acc[r] ^= v;
+        continue;
+      }
+      const uint8_t* t = lut + (r * K + j) * 32;
+      acc[r].x ^= gf_mul_lds(t, lo.x, hi.x);
+      acc[r].y ^= gf_mul_lds(t, lo.y, hi.y);
+      acc[r].z ^= gf_mul_lds(t, lo.z, hi.z);
+      acc[r].w ^= gf_mul_lds(t, lo.w, hi.w);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], a.nt);
+}
+
+// ------------------------------------------- generic K (> kMaxSpecK) ----
+template <int R>
+__global__ __launch_bounds__(kBlock) void gf_apply_perm_generic(ApplyArgs a) {
+  const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+  u32x4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+  const int K = a.K;
+  int j = 0;
+  for (; j + 4 <= K; j += 4) {
+    u32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = load16(sp[j + u], col, a.nt);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const u32x4 v = x[u];
+      const u32x4 s0 = v & kLo2, s1 = (v >> 2) & kLo2, s2 = (v >> 4) & kLo2, s3 = (v >> 6) & kLo2;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u32x4 q = a.qtab[r * K + j + u];
+        if (q.x == 0u) continue;
+        if (q.x == kQ0Unit) {
+          acc[r] ^= v;
+          continue;
+        }
+        acc[r].x ^= gf_mul_perm(q, s0.x, s1.x, s2.x, s3.x);
+        acc[r].y ^= gf_mul_perm(q, s0.y, s1.y, s2.y, s3.y);
+        acc[r].z ^= gf_mul_perm(q, s0.z, s1.z, s2.z, s3.z);
+        acc[r].w ^= gf_mul_perm(q, s0.w, s1.w, s2.w, s3.w);
+      }
+    }
+  }
+  for (; j < K; ++j) {
+    const u32x4 v = load16(sp[j], col, a.nt);
+    const u32x4 s0 = v & kLo2, s1 = (v >> 2) & kLo2, s2 = (v >> 4) & kLo2, s3 = (v >> 6) & kLo2;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u32x4 q = a.qtab[r * K + j];
+      acc[r].x ^= gf_mul_perm(q, s0.x, s1.x, s2.x, s3.x);
+      acc[r].y ^= gf_mul_perm(q, s0.y, s1.y, s2.y, s3.y);
+      acc[r].z ^= gf_mul_perm(q, s0.z, s1.z, s2.z, s3.z);
+      acc[r].w ^= gf_mul_perm(q, s0.w, s1.w, s2.w, s3.w);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], a.nt);
+}
+
+// --------------------------------------- bytes: tails, misaligned shards ----
+// One lane per byte in [byte0, size); any K, R <= kMaxRows, any alignment.
+__global__ __launch_bounds__(kBlock) void gf_apply_bytes(ApplyArgs a) {
+  const int64_t x = a.byte0 + int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (x >= a.size) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+  uint32_t acc[kMaxRows] = {0u, 0u, 0u, 0u};
+  for (int j = 0; j < a.K; ++j) {
+    const uint32_t v = sp[j][x];
+    const uint32_t s0 = v & 3u, s1 = (v >> 2) & 3u, s2 = (v >> 4) & 3u, s3 = v >> 6;
+    for (int r = 0; r < a.R; ++r) acc[r] ^= gf_mul_perm(a.qtab[r * a.K + j], s0, s1, s2, s3);
+  }
+  for (int r = 0; r < a.R; ++r) dp[r][x] = uint8_t(acc[r]);
+}
+
+}  // namespace dev
+}  // namespace ecgpu

@@ -1,0 +1,185 @@
+// jerasure_dropin.cpp -- libjerasure_amd.so: the reference's C++ coding
+// surface (include/dropin/*.h == reference include/{galois,jerasure,
+// reed_sol}.h signatures, C++ linkage) on top of libecgpu.so.
+//
+// Callers such as the reference's client (client_main.cpp:1060, :2118) and
+// ECX datanode (ecx_datanode_main.cpp:714, :724, :1391) link this library in
+// place of src/erasure_coding/*.cpp.  The w = 8 hot path -- matrix encode,
+// decode, dot product, region multiply / XOR, parity, RAID-6 -- runs on the
+// MI355X through include/ecgpu.h; a GPU failure is fatal (message + abort),
+// never a silent CPU fallback.  Host-side math (fields, matrices) comes from
+// libecgpu's host C ABI.  The surface the north star does not cover (w = 16
+// / 32 regions, bit-matrix / schedule coding) is CPU code in
+// jerasure_surface.cpp.
+#include <cstdio>
+#include <cstdlib>
+
+#include "ecgpu.h"
+// The reference surface is this library's export list (default visibility);
+// everything else is built -fvisibility=hidden.
+#pragma GCC visibility push(default)
+#include "galois.h"
+#include "jerasure.h"
+#include "reed_sol.h"
+#pragma GCC visibility pop
+#include "surface_cpu.hpp"
+
+namespace {
+
+[[noreturn]] void gpu_fatal(const char* fn, int rc) {
+  std::fprintf(stderr, "%s: MI355X path failed (%d): %s\n", fn, rc, ecgpu_last_error());
+  std::abort();
+}
+
+inline void check(const char* fn, int rc) {
+  if (rc != ECGPU_OK) gpu_fatal(fn, rc);
+}
+
+}  // namespace
+
+// ============================================================ galois.h ====
+int galois_single_multiply(int a, int b, int w) { return ecgpu_galois_single_multiply(a, b, w); }
+int galois_single_divide(int a, int b, int w) { return ecgpu_galois_single_divide(a, b, w); }
+int galois_inverse(int x, int w) { return ecgpu_galois_inverse(x, w); }
+
+int galois_log(int value, int w) {
+  if (w > 30) {
+    std::fprintf(stderr, "Error: galois_log - w is too big.  Sorry\n");
+    std::exit(1);
+  }
+  return ecgpu_galois_log(value, w);
+}
+
+int galois_ilog(int value, int w) {
+  if (w > 30) {
+    std::fprintf(stderr, "Error: galois_ilog - w is too big.  Sorry\n");
+    std::exit(1);
+  }
+  return ecgpu_galois_ilog(value, w);
+}
+
+int galois_create_log_tables(int w) { return ecgpu_cpu::create_log_tables(w); }
+int galois_create_mult_tables(int w) { return ecgpu_cpu::create_mult_tables(w); }
+int galois_create_split_w8_tables() { return 0; }  // w=32 multiply needs no tables here
+
+int galois_logtable_multiply(int x, int y, int w) { return (x == 0 || y == 0) ? 0 : ecgpu_galois_single_multiply(x, y, w); }
+int galois_logtable_divide(int x, int y, int w) { return ecgpu_galois_single_divide(x, y, w); }
+int galois_multtable_multiply(int x, int y, int w) { return ecgpu_galois_single_multiply(x, y, w); }
+int galois_multtable_divide(int x, int y, int w) { return ecgpu_galois_single_divide(x, y, w); }
+int galois_shift_multiply(int x, int y, int w) { return ecgpu_cpu::shift_multiply(x, y, w); }
+int galois_shift_divide(int a, int b, int w) {
+  if (b == 0) return -1;
+  if (a == 0) return 0;
+  return ecgpu_cpu::shift_multiply(a, ecgpu_cpu::shift_inverse(b, w), w);
+}
+int galois_shift_inverse(int y, int w) { return ecgpu_cpu::shift_inverse(y, w); }
+int galois_split_w8_multiply(int x, int y) { return ecgpu_cpu::shift_multiply(x, y, 32); }
+
+int* galois_get_mult_table(int w) { return ecgpu_cpu::mult_table(w); }
+int* galois_get_div_table(int w) { return ecgpu_cpu::div_table(w); }
+int* galois_get_log_table(int w) { return ecgpu_cpu::log_table(w); }
+int* galois_get_ilog_table(int w) { return ecgpu_cpu::ilog_table(w); }
+
+void galois_region_xor(char* r1, char* r2, char* r3, int nbytes) {
+  check("galois_region_xor", ecgpu_galois_region_xor(r1, r2, r3, nbytes));
+}
+
+void galois_w08_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
+  check("galois_w08_region_multiply", ecgpu_galois_w08_region_multiply(region, multby, nbytes, r2, add));
+}
+
+void galois_w16_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
+  ecgpu_cpu::region_multiply_w16(region, multby, nbytes, r2, add);
+}
+
+void galois_w32_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
+  ecgpu_cpu::region_multiply_w32(region, multby, nbytes, r2, add);
+}
+
+// ========================================================== reed_sol.h ====
+int* reed_sol_vandermonde_coding_matrix(int k, int m, int w) { return ecgpu_reed_sol_vandermonde_coding_matrix(k, m, w); }
+int* reed_sol_extended_vandermonde_matrix(int rows, int cols, int w) {
+  return ecgpu_reed_sol_extended_vandermonde_matrix(rows, cols, w);
+}
+int* reed_sol_big_vandermonde_distribution_matrix(int rows, int cols, int w) {
+  return ecgpu_reed_sol_big_vandermonde_distribution_matrix(rows, cols, w);
+}
+int* reed_sol_r6_coding_matrix(int k, int w) { return ecgpu_reed_sol_r6_coding_matrix(k, w); }
+
+int reed_sol_r6_encode(int k, int w, char** data_ptrs, char** coding_ptrs, int size) {
+  if (w == 8) {
+    const int rc = ecgpu_reed_sol_r6_encode(k, w, data_ptrs, coding_ptrs, size);
+    if (rc < 0) gpu_fatal("reed_sol_r6_encode", rc);
+    return rc;
+  }
+  return ecgpu_cpu::r6_encode(k, w, data_ptrs, coding_ptrs, size);
+}
+
+void reed_sol_galois_w08_region_multby_2(char* region, int nbytes) {
+  check("reed_sol_galois_w08_region_multby_2", ecgpu_reed_sol_galois_w08_region_multby_2(region, nbytes));
+}
+void reed_sol_galois_w16_region_multby_2(char* region, int nbytes) {
+  ecgpu_cpu::region_multiply_w16(region, 2, nbytes, nullptr, 0);
+}
+void reed_sol_galois_w32_region_multby_2(char* region, int nbytes) {
+  ecgpu_cpu::region_multiply_w32(region, 2, nbytes, nullptr, 0);
+}
+
+// ========================================================== jerasure.h ====
+void jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs, int size) {
+  if (w != 8 && w != 16 && w != 32) {
+    std::fprintf(stderr, "ERROR: jerasure_matrix_encode() and w is not 8, 16 or 32\n");
+    std::exit(1);
+  }
+  if (w == 8) {
+    check("jerasure_matrix_encode", ecgpu_jerasure_matrix_encode(k, m, w, matrix, data_ptrs, coding_ptrs, size));
+    return;
+  }
+  for (int i = 0; i < m; ++i)
+    ecgpu_cpu::matrix_dotprod(k, w, matrix + i * k, nullptr, k + i, data_ptrs, coding_ptrs, size);
+}
+
+int jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
+                           char** coding_ptrs, int size) {
+  if (w != 8 && w != 16 && w != 32) return -1;
+  if (w != 8) return ecgpu_cpu::matrix_decode(k, m, w, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size);
+  const int rc = ecgpu_jerasure_matrix_decode(k, m, w, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size);
+  if (rc == ECGPU_ERR) return -1;
+  check("jerasure_matrix_decode", rc);
+  return 0;
+}
+
+void jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int dest_id, char** data_ptrs,
+                             char** coding_ptrs, int size) {
+  if (w != 1 && w != 8 && w != 16 && w != 32) {
+    std::fprintf(stderr, "ERROR: jerasure_matrix_dotprod() called and w is not 1, 8, 16 or 32\n");
+    std::exit(1);
+  }
+  if (w == 8) {
+    check("jerasure_matrix_dotprod",
+          ecgpu_jerasure_matrix_dotprod(k, w, matrix_row, src_ids, dest_id, data_ptrs, coding_ptrs, size));
+    return;
+  }
+  ecgpu_cpu::matrix_dotprod(k, w, matrix_row, src_ids, dest_id, data_ptrs, coding_ptrs, size);
+}
+
+void jerasure_do_parity(int k, char** data_ptrs, char* parity_ptr, int size) {
+  check("jerasure_do_parity", ecgpu_jerasure_do_parity(k, data_ptrs, parity_ptr, size));
+}
+
+int jerasure_make_decoding_matrix(int k, int m, int w, int* matrix, int* erased, int* decoding_matrix, int* dm_ids) {
+  return ecgpu_jerasure_make_decoding_matrix(k, m, w, matrix, erased, decoding_matrix, dm_ids);
+}
+int* jerasure_erasures_to_erased(int k, int m, int* erasures) { return ecgpu_jerasure_erasures_to_erased(k, m, erasures); }
+int jerasure_invert_matrix(int* mat, int* inv, int rows, int w) { return ecgpu_jerasure_invert_matrix(mat, inv, rows, w); }
+int jerasure_invertible_matrix(int* mat, int rows, int w) { return ecgpu_jerasure_invertible_matrix(mat, rows, w); }
+int* jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, int r2, int c2, int w) {
+  return ecgpu_jerasure_matrix_multiply(m1, m2, r1, c1, r2, c2, w);
+}
+
+void jerasure_get_stats(double* fill_in) {
+  ecgpu_jerasure_get_stats(fill_in);  // GPU-path counters (reset)
+  double cpu[3];
+  ecgpu_cpu::take_stats(cpu);          // CPU-surface counters (reset)
+  for (int i = 0; i < 3; ++i) fill_in[i] += cpu[i];
+}

@@ -1,0 +1,587 @@
+// jerasure_surface.cpp -- CPU implementation of the reference surface that
+// lies outside the north-star GF(2^8) path: w = 16 / 32 region math and
+// matrix coding, GF(2) bit-matrix coding and XOR schedules
+// (jerasure.cpp:257-345, :623-1032, :1153-1344), matrix printing.  These
+// keep include/dropin/jerasure.h link- and behaviour-compatible; none of the
+// reference's callers uses them.
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "gf_host.hpp"
+// The reference surface is this library's export list (default visibility);
+// everything else is built -fvisibility=hidden.
+#pragma GCC visibility push(default)
+#include "jerasure.h"
+#pragma GCC visibility pop
+#include "matrix_host.hpp"
+#include "surface_cpu.hpp"
+
+namespace ecgpu_cpu {
+
+namespace {
+std::mutex g_mu;
+double g_stats[3] = {0, 0, 0};
+
+inline char* dev_ptr(int id, int k, char** data, char** coding) { return id < k ? data[id] : coding[id - k]; }
+}  // namespace
+
+int create_log_tables(int w) { return ecgpu::create_log_tables(w); }
+int create_mult_tables(int w) { return ecgpu::create_mult_tables(w); }
+int* mult_table(int w) { return ecgpu::mult_table(w); }
+int* div_table(int w) { return ecgpu::div_table(w); }
+int* log_table(int w) { return ecgpu::log_table(w); }
+int* ilog_table(int w) { return ecgpu::ilog_table(w); }
+int shift_multiply(int a, int b, int w) { return ecgpu::shift_multiply(a, b, w); }
+int shift_inverse(int a, int w) { return ecgpu::shift_inverse(a, w); }
+
+void count(double x, double g, double m) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_stats[0] += x;
+  g_stats[1] += g;
+  g_stats[2] += m;
+}
+
+void take_stats(double out[3]) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int i = 0; i < 3; ++i) {
+    out[i] = g_stats[i];
+    g_stats[i] = 0;
+  }
+}
+
+void region_xor(const char* r1, const char* r2, char* r3, long n) {
+  for (long i = 0; i < n; ++i) r3[i] = char(r1[i] ^ r2[i]);
+}
+
+void region_multiply_w16(char* region, int multby, int nbytes, char* r2, int add) {
+  uint16_t* src = reinterpret_cast<uint16_t*>(region);
+  uint16_t* dst = reinterpret_cast<uint16_t*>(r2 ? r2 : region);
+  const int n = nbytes / 2;
+  if (multby == 0) {  // galois.cpp:499-507
+    if (!add) std::memset(dst, 0, size_t(n) * 2);
+    return;
+  }
+  const bool acc = r2 != nullptr && add;
+  for (int i = 0; i < n; ++i) {
+    const uint16_t p = uint16_t(ecgpu::single_multiply(src[i], multby, 16));
+    dst[i] = acc ? uint16_t(dst[i] ^ p) : p;
+  }
+}
+
+void region_multiply_w32(char* region, int multby, int nbytes, char* r2, int add) {
+  uint32_t* src = reinterpret_cast<uint32_t*>(region);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(r2 ? r2 : region);
+  const int n = nbytes / 4;
+  for (int i = 0; i < n; ++i) {  // galois.cpp:698-726: add applies even in place
+    const uint32_t p = ecgpu::gf_mul_poly(src[i], uint32_t(multby), 32);
+    dst[i] = add ? (dst[i] ^ p) : p;
+  }
+}
+
+void matrix_dotprod(int k, int w, const int* row, const int* src_ids, int dest_id, char** data, char** coding,
+                    int size) {
+  char* dst = dev_ptr(dest_id, k, data, coding);
+  auto src = [&](int i) { return src_ids ? dev_ptr(src_ids[i], k, data, coding) : data[i]; };
+  bool init = false;
+  for (int i = 0; i < k; ++i) {
+    if (row[i] != 1) continue;
+    if (!init) {
+      std::memcpy(dst, src(i), size_t(size));
+      count(0, 0, size);
+      init = true;
+    } else {
+      region_xor(src(i), dst, dst, size);
+      count(size, 0, 0);
+    }
+  }
+  for (int i = 0; i < k; ++i) {
+    if (row[i] == 0 || row[i] == 1) continue;
+    if (w == 16) region_multiply_w16(src(i), row[i], size, dst, init);
+    if (w == 32) region_multiply_w32(src(i), row[i], size, dst, init);
+    count(0, size, 0);
+    init = true;
+  }
+}
+
+int matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data, char** coding,
+                  int size) {
+  int* erased = ecgpu::erasures_to_erased(k, m, erasures);
+  if (!erased) return -1;
+  int edd = 0, lastdrive = k;
+  for (int i = 0; i < k; ++i)
+    if (erased[i]) {
+      ++edd;
+      lastdrive = i;
+    }
+  if (!row_k_ones || erased[k]) lastdrive = k;
+  std::vector<int> dm, ids;
+  if (edd > 1 || (edd > 0 && (!row_k_ones || erased[k]))) {
+    dm.resize(size_t(k) * k);
+    ids.resize(size_t(k));
+    if (ecgpu::make_decoding_matrix(k, m, w, matrix, erased, dm.data(), ids.data()) < 0) {
+      std::free(erased);
+      return -1;
+    }
+  }
+  for (int i = 0; edd > 0 && i < lastdrive; ++i)
+    if (erased[i]) {
+      matrix_dotprod(k, w, dm.data() + size_t(i) * k, ids.data(), i, data, coding, size);
+      --edd;
+    }
+  if (edd > 0) {
+    std::vector<int> t(static_cast<size_t>(k));
+    for (int i = 0; i < k; ++i) t[i] = i < lastdrive ? i : i + 1;
+    matrix_dotprod(k, w, matrix, t.data(), lastdrive, data, coding, size);
+  }
+  for (int i = 0; i < m; ++i)
+    if (erased[k + i]) matrix_dotprod(k, w, matrix + size_t(i) * k, nullptr, k + i, data, coding, size);
+  std::free(erased);
+  return 0;
+}
+
+int r6_encode(int k, int w, char** data, char** coding, int size) {
+  if (w != 16 && w != 32) return 0;
+  std::memcpy(coding[0], data[0], size_t(size));
+  for (int i = 1; i < k; ++i) region_xor(coding[0], data[i], coding[0], size);
+  std::memcpy(coding[1], data[k - 1], size_t(size));
+  for (int i = k - 2; i >= 0; --i) {
+    if (w == 16) region_multiply_w16(coding[1], 2, size, nullptr, 0);
+    else region_multiply_w32(coding[1], 2, size, nullptr, 0);
+    region_xor(coding[1], data[i], coding[1], size);
+  }
+  return 1;
+}
+
+}  // namespace ecgpu_cpu
+
+using ecgpu_cpu::count;
+using ecgpu_cpu::region_xor;
+
+// ===================================================== bit-matrices ====
+int* jerasure_matrix_to_bitmatrix(int k, int m, int w, int* matrix) {
+  return ecgpu::matrix_to_bitmatrix(k, m, w, matrix);
+}
+int jerasure_invert_bitmatrix(int* mat, int* inv, int rows) { return ecgpu::invert_bitmatrix(mat, inv, rows); }
+int jerasure_invertible_bitmatrix(int* mat, int rows) { return ecgpu::invertible_bitmatrix(mat, rows); }
+int jerasure_make_decoding_bitmatrix(int k, int m, int w, int* matrix, int* erased, int* dm, int* dm_ids) {
+  return ecgpu::make_decoding_bitmatrix(k, m, w, matrix, erased, dm, dm_ids);
+}
+
+// One output device = w packets; packet j of the output is the XOR of the
+// source packets whose bit is set in row j of the device's w x k*w block.
+void jerasure_bitmatrix_dotprod(int k, int w, int* bm_row, int* src_ids, int dest_id, char** data, char** coding,
+                                int size, int packetsize) {
+  const int chunk = w * packetsize;
+  if (size % chunk != 0) {
+    std::fprintf(stderr, "jerasure_bitmatrix_dotprod - size%%(w*packetsize)) must = 0\n");
+    std::exit(1);
+  }
+  char* out = dest_id < k ? data[dest_id] : coding[dest_id - k];
+  for (int off = 0; off < size; off += chunk) {
+    const int* bit = bm_row;
+    for (int j = 0; j < w; ++j) {
+      char* dst = out + off + j * packetsize;
+      bool started = false;
+      for (int x = 0; x < k; ++x) {
+        char* base = !src_ids ? data[x] : (src_ids[x] < k ? data[src_ids[x]] : coding[src_ids[x] - k]);
+        for (int y = 0; y < w; ++y, ++bit) {
+          if (!*bit) continue;
+          const char* s = base + off + y * packetsize;
+          if (!started) {
+            std::memcpy(dst, s, size_t(packetsize));
+            count(0, 0, packetsize);
+            started = true;
+          } else {
+            region_xor(dst, s, dst, packetsize);
+            count(packetsize, 0, 0);
+          }
+        }
+      }
+    }
+  }
+}
+
+void jerasure_bitmatrix_encode(int k, int m, int w, int* bitmatrix, char** data, char** coding, int size,
+                               int packetsize) {
+  if (packetsize % int(sizeof(long)) != 0) {
+    std::fprintf(stderr, "jerasure_bitmatrix_encode - packetsize(%d) %% sizeof(long) != 0\n", packetsize);
+    std::exit(1);
+  }
+  if (size % (packetsize * w) != 0) {
+    std::fprintf(stderr, "jerasure_bitmatrix_encode - size(%d) %% (packetsize(%d)*w(%d))) != 0\n", size,
+                 packetsize, w);
+    std::exit(1);
+  }
+  for (int i = 0; i < m; ++i)
+    jerasure_bitmatrix_dotprod(k, w, bitmatrix + size_t(i) * k * w * w, nullptr, k + i, data, coding, size,
+                               packetsize);
+}
+
+int jerasure_bitmatrix_decode(int k, int m, int w, int* bitmatrix, int row_k_ones, int* erasures, char** data,
+                              char** coding, int size, int packetsize) {
+  int* erased = ecgpu::erasures_to_erased(k, m, erasures);
+  if (!erased) return -1;
+  int edd = 0, lastdrive = k;
+  for (int i = 0; i < k; ++i)
+    if (erased[i]) {
+      ++edd;
+      lastdrive = i;
+    }
+  if (row_k_ones != 1 || erased[k]) lastdrive = k;
+  const size_t blk = size_t(k) * w * w;
+  std::vector<int> dm, ids;
+  if (edd > 1 || (edd > 0 && (row_k_ones != 1 || erased[k]))) {
+    dm.resize(blk * k);
+    ids.resize(size_t(k));
+    if (ecgpu::make_decoding_bitmatrix(k, m, w, bitmatrix, erased, dm.data(), ids.data()) < 0) {
+      std::free(erased);
+      return -1;
+    }
+  }
+  for (int i = 0; edd > 0 && i < lastdrive; ++i)
+    if (erased[i]) {
+      jerasure_bitmatrix_dotprod(k, w, dm.data() + i * blk, ids.data(), i, data, coding, size, packetsize);
+      --edd;
+    }
+  if (edd > 0) {
+    std::vector<int> t(static_cast<size_t>(k));
+    for (int i = 0; i < k; ++i) t[i] = i < lastdrive ? i : i + 1;
+    jerasure_bitmatrix_dotprod(k, w, bitmatrix, t.data(), lastdrive, data, coding, size, packetsize);
+  }
+  for (int i = 0; i < m; ++i)
+    if (erased[k + i])
+      jerasure_bitmatrix_dotprod(k, w, bitmatrix + i * blk, nullptr, k + i, data, coding, size, packetsize);
+  std::free(erased);
+  return 0;
+}
+
+// ======================================================== schedules ====
+// An op is 5 ints {src dev, src packet, dst dev, dst packet, xor?}; a
+// schedule is a malloc'd array of malloc'd ops ending with op[0] == -1.
+namespace {
+int* make_op(int sd, int sp, int dd, int dp, int x) {
+  int* o = static_cast<int*>(std::malloc(5 * sizeof(int)));
+  o[0] = sd;
+  o[1] = sp;
+  o[2] = dd;
+  o[3] = dp;
+  o[4] = x;
+  return o;
+}
+int* end_op() {
+  int* o = static_cast<int*>(std::malloc(5 * sizeof(int)));
+  o[0] = -1;
+  return o;
+}
+}  // namespace
+
+int** jerasure_dumb_bitmatrix_to_schedule(int k, int m, int w, int* bitmatrix) {
+  int** ops = static_cast<int**>(std::malloc(sizeof(int*) * (size_t(k) * m * w * w + 1)));
+  int n = 0;
+  const int cols = k * w;
+  for (int r = 0; r < m * w; ++r) {
+    int xor_flag = 0;
+    for (int c = 0; c < cols; ++c)
+      if (bitmatrix[r * cols + c]) {
+        ops[n++] = make_op(c / w, c % w, k + r / w, r % w, xor_flag);
+        xor_flag = 1;
+      }
+  }
+  ops[n] = end_op();
+  return ops;
+}
+
+// Greedy reuse: repeatedly emit the pending row that is cheapest to build,
+// either from scratch (popcount) or as a copy of an already-built row plus
+// the XOR of the differing bits (1 + Hamming distance).
+int** jerasure_smart_bitmatrix_to_schedule(int k, int m, int w, int* bitmatrix) {
+  const int rows = m * w, cols = k * w;
+  int** ops = static_cast<int**>(std::malloc(sizeof(int*) * (size_t(k) * m * w * w + 1)));
+  int n = 0;
+  std::vector<int> cost(static_cast<size_t>(rows)), from(static_cast<size_t>(rows), -1),
+      next(static_cast<size_t>(rows)), prev(static_cast<size_t>(rows));
+  int best = 0, best_cost = cols + 1;
+  for (int r = 0; r < rows; ++r) {
+    int pop = 0;
+    for (int c = 0; c < cols; ++c) pop += bitmatrix[r * cols + c];
+    cost[r] = pop;
+    next[r] = r + 1;
+    prev[r] = r - 1;
+    if (pop < best_cost) {
+      best_cost = pop;
+      best = r;
+    }
+  }
+  next[rows - 1] = -1;
+  int head = 0;
+  while (head != -1) {
+    const int row = best;
+    if (prev[row] == -1) {  // unlink row from the pending list
+      head = next[row];
+      if (head != -1) prev[head] = -1;
+    } else {
+      next[prev[row]] = next[row];
+      if (next[row] != -1) prev[next[row]] = prev[row];
+    }
+    const int* bits = bitmatrix + row * cols;
+    if (from[row] == -1) {
+      int xor_flag = 0;
+      for (int c = 0; c < cols; ++c)
+        if (bits[c]) {
+          ops[n++] = make_op(c / w, c % w, k + row / w, row % w, xor_flag);
+          xor_flag = 1;
+        }
+    } else {
+      ops[n++] = make_op(k + from[row] / w, from[row] % w, k + row / w, row % w, 0);
+      const int* base = bitmatrix + from[row] * cols;
+      for (int c = 0; c < cols; ++c)
+        if (bits[c] ^ base[c]) ops[n++] = make_op(c / w, c % w, k + row / w, row % w, 1);
+    }
+    best_cost = cols + 1;
+    for (int r = head; r != -1; r = next[r]) {
+      int d = 1;
+      const int* other = bitmatrix + r * cols;
+      for (int c = 0; c < cols; ++c) d += bits[c] ^ other[c];
+      if (d < cost[r]) {
+        from[r] = row;
+        cost[r] = d;
+      }
+      if (cost[r] < best_cost) {
+        best_cost = cost[r];
+        best = r;
+      }
+    }
+  }
+  ops[n] = end_op();
+  return ops;
+}
+
+void jerasure_free_schedule(int** schedule) {
+  int i = 0;
+  for (; schedule[i][0] >= 0; ++i) std::free(schedule[i]);
+  std::free(schedule[i]);
+  std::free(schedule);
+}
+
+void jerasure_do_scheduled_operations(char** ptrs, int** ops, int packetsize) {
+  for (int i = 0; ops[i][0] >= 0; ++i) {
+    const int* o = ops[i];
+    char* s = ptrs[o[0]] + o[1] * packetsize;
+    char* d = ptrs[o[2]] + o[3] * packetsize;
+    if (o[4]) {
+      region_xor(s, d, d, packetsize);
+      count(packetsize, 0, 0);
+    } else {
+      std::memcpy(d, s, size_t(packetsize));
+      count(0, 0, packetsize);
+    }
+  }
+}
+
+void jerasure_schedule_encode(int k, int m, int w, int** schedule, char** data, char** coding, int size,
+                              int packetsize) {
+  std::vector<char*> p(static_cast<size_t>(k + m));
+  for (int i = 0; i < k; ++i) p[i] = data[i];
+  for (int i = 0; i < m; ++i) p[k + i] = coding[i];
+  for (int done = 0; done < size; done += packetsize * w) {
+    jerasure_do_scheduled_operations(p.data(), schedule, packetsize);
+    for (auto& q : p) q += packetsize * w;
+  }
+}
+
+namespace {
+
+// Survivor/erased layout for scheduled decoding (jerasure.cpp:705-803):
+// slot i < k holds data i, or -- if data i is erased -- the lowest unused
+// surviving coding device; slots k.. hold the erased data then the erased
+// coding devices.  row_ids[slot] = device id, ind_to_row[device] = slot.
+bool schedule_layout(int k, int m, const int* erasures, std::vector<int>& row_ids, std::vector<int>& ind_to_row) {
+  int* erased = ecgpu::erasures_to_erased(k, m, erasures);
+  if (!erased) return false;
+  row_ids.assign(size_t(k + m), 0);
+  ind_to_row.assign(size_t(k + m), 0);
+  int j = k, x = k;
+  for (int i = 0; i < k; ++i) {
+    if (!erased[i]) {
+      row_ids[i] = i;
+      ind_to_row[i] = i;
+    } else {
+      while (erased[j]) ++j;
+      row_ids[i] = j;
+      ind_to_row[j] = i;
+      ++j;
+      row_ids[x] = i;
+      ind_to_row[i] = x;
+      ++x;
+    }
+  }
+  for (int i = k; i < k + m; ++i)
+    if (erased[i]) {
+      row_ids[x] = i;
+      ind_to_row[i] = x;
+      ++x;
+    }
+  std::free(erased);
+  return true;
+}
+
+char** schedule_ptrs(int k, int m, const int* erasures, char** data, char** coding) {
+  std::vector<int> row_ids, ind;
+  if (!schedule_layout(k, m, erasures, row_ids, ind)) return nullptr;
+  char** p = static_cast<char**>(std::malloc(sizeof(char*) * size_t(k + m)));
+  int nerased = 0;
+  for (int i = 0; erasures[i] != -1; ++i) ++nerased;
+  for (int s = 0; s < k + m; ++s) {
+    if (s >= k && s - k >= nerased) {
+      p[s] = nullptr;
+      continue;
+    }
+    const int id = row_ids[s];
+    p[s] = id < k ? data[id] : coding[id - k];
+  }
+  return p;
+}
+
+// One bit-matrix that rebuilds every erased device in one schedule.
+int** decoding_schedule(int k, int m, int w, const int* bitmatrix, const int* erasures, int smart) {
+  int ddf = 0, cdf = 0;
+  for (int i = 0; erasures[i] != -1; ++i) (erasures[i] < k ? ddf : cdf)++;
+  std::vector<int> row_ids, ind;
+  if (!schedule_layout(k, m, erasures, row_ids, ind)) return nullptr;
+  const int kw = k * w;
+  const size_t blk = size_t(kw) * w;
+  std::vector<int> real(blk * size_t(ddf + cdf), 0);
+  if (ddf > 0) {
+    std::vector<int> sys(blk * k, 0), inv(blk * k, 0);
+    for (int i = 0; i < k; ++i) {
+      int* b = &sys[i * blk];
+      if (row_ids[i] == i)
+        for (int x = 0; x < w; ++x) b[x * kw + i * w + x] = 1;
+      else
+        std::memcpy(b, bitmatrix + blk * (row_ids[i] - k), sizeof(int) * blk);
+    }
+    ecgpu::invert_bitmatrix(sys.data(), inv.data(), kw);
+    for (int i = 0; i < ddf; ++i) std::memcpy(&real[i * blk], &inv[blk * row_ids[k + i]], sizeof(int) * blk);
+  }
+  for (int x = 0; x < cdf; ++x) {
+    const int drive = row_ids[x + ddf + k] - k;
+    int* out = &real[blk * (ddf + x)];
+    const int* coding_blk = bitmatrix + blk * drive;
+    std::memcpy(out, coding_blk, sizeof(int) * blk);
+    for (int i = 0; i < k; ++i)  // erased data columns are re-expressed ...
+      if (row_ids[i] != i)
+        for (int j = 0; j < w; ++j) std::memset(out + j * kw + i * w, 0, sizeof(int) * w);
+    for (int i = 0; i < k; ++i) {  // ... through the decoding rows of that data device
+      if (row_ids[i] == i) continue;
+      const int* dec = &real[blk * (ind[i] - k)];
+      for (int j = 0; j < w; ++j)
+        for (int y = 0; y < w; ++y)
+          if (coding_blk[j * kw + i * w + y])
+            for (int z = 0; z < kw; ++z) out[j * kw + z] ^= dec[z + y * kw];
+    }
+  }
+  return smart ? jerasure_smart_bitmatrix_to_schedule(k, ddf + cdf, w, real.data())
+               : jerasure_dumb_bitmatrix_to_schedule(k, ddf + cdf, w, real.data());
+}
+
+void run_schedule(int k, int m, int w, int** schedule, char** ptrs, int size, int packetsize) {
+  for (int done = 0; done < size; done += packetsize * w) {
+    jerasure_do_scheduled_operations(ptrs, schedule, packetsize);
+    for (int i = 0; i < k + m; ++i)
+      if (ptrs[i]) ptrs[i] += packetsize * w;
+  }
+}
+
+}  // namespace
+
+int jerasure_schedule_decode_lazy(int k, int m, int w, int* bitmatrix, int* erasures, char** data, char** coding,
+                                  int size, int packetsize, int smart) {
+  char** ptrs = schedule_ptrs(k, m, erasures, data, coding);
+  if (!ptrs) return -1;
+  int** sched = decoding_schedule(k, m, w, bitmatrix, erasures, smart);
+  if (!sched) {
+    std::free(ptrs);
+    return -1;
+  }
+  run_schedule(k, m, w, sched, ptrs, size, packetsize);
+  jerasure_free_schedule(sched);
+  std::free(ptrs);
+  return 0;
+}
+
+int jerasure_schedule_decode_cache(int k, int m, int w, int*** scache, int* erasures, char** data, char** coding,
+                                   int size, int packetsize) {
+  int index;
+  if (erasures[1] == -1)
+    index = erasures[0] * (k + m) + erasures[0];
+  else if (erasures[2] == -1)
+    index = erasures[0] * (k + m) + erasures[1];
+  else
+    return -1;
+  char** ptrs = schedule_ptrs(k, m, erasures, data, coding);
+  if (!ptrs) return -1;
+  run_schedule(k, m, w, scache[index], ptrs, size, packetsize);
+  std::free(ptrs);
+  return 0;
+}
+
+int*** jerasure_generate_schedule_cache(int k, int m, int w, int* bitmatrix, int smart) {
+  if (m != 2) return nullptr;
+  const int n = k + m;
+  int*** cache = static_cast<int***>(std::calloc(size_t(n) * (n + 1), sizeof(int**)));
+  if (!cache) return nullptr;
+  for (int e1 = 0; e1 < n; ++e1) {
+    for (int e2 = 0; e2 < e1; ++e2) {
+      const int er[3] = {e1, e2, -1};
+      cache[e1 * n + e2] = decoding_schedule(k, m, w, bitmatrix, er, smart);
+      cache[e2 * n + e1] = cache[e1 * n + e2];
+    }
+    const int er[2] = {e1, -1};
+    cache[e1 * n + e1] = decoding_schedule(k, m, w, bitmatrix, er, smart);
+  }
+  return cache;
+}
+
+void jerasure_free_schedule_cache(int k, int m, int*** cache) {
+  if (m != 2) {
+    std::fprintf(stderr, "jerasure_free_schedule_cache(): m must equal 2\n");
+    std::exit(1);
+  }
+  const int n = k + m;
+  for (int e1 = 0; e1 < n; ++e1) {
+    for (int e2 = 0; e2 < e1; ++e2) jerasure_free_schedule(cache[e1 * n + e2]);
+    jerasure_free_schedule(cache[e1 * n + e1]);
+  }
+  std::free(cache);
+}
+
+// ========================================================= printing ====
+void jerasure_print_matrix(int* mtx, int rows, int cols, int w) {
+  int width = 10;
+  if (w != 32) {
+    char buf[32];
+    width = std::snprintf(buf, sizeof buf, "%u", (1u << w) - 1u);
+  }
+  for (int i = 0; i < rows; ++i) {
+    for (int j = 0; j < cols; ++j) {
+      if (j) std::printf(" ");
+      std::printf("%*u", width, unsigned(mtx[i * cols + j]));
+    }
+    std::printf("\n");
+  }
+}
+
+void jerasure_print_bitmatrix(int* mtx, int rows, int cols, int w) {
+  for (int i = 0; i < rows; ++i) {
+    if (i && i % w == 0) std::printf("\n");
+    for (int j = 0; j < cols; ++j) {
+      if (j && j % w == 0) std::printf(" ");
+      std::printf("%d", mtx[i * cols + j]);
+    }
+    std::printf("\n");
+  }
+}

@@ -1,0 +1,71 @@
+// planner.hpp -- symbolic replay of the reference's region-op sequences.
+//
+// The reference computes encode/decode as a SEQUENCE of whole-region ops
+// (memcpy, XOR, multiply-add) over caller buffers (jerasure.cpp:561-620,
+// :153-254).  Every op is GF(2^8)-linear, so the final content of each
+// written buffer is a fixed linear combination of the ORIGINAL contents of
+// the buffers involved.  The tracker replays the sequence on coefficient
+// vectors (one per buffer, indexed by buffer identity = pointer) and emits a
+// single fused op: outputs x sources coefficient matrix.  One GPU launch then
+// reads every source once and writes every output once -- bit-identical to the
+// sequential reference, including aliasing (a destination that is also a
+// source) and the "all-zero row leaves the destination untouched" rule.
+#pragma once
+#include <cstdint>
+#include <unordered_map>
+#include <vector>
+
+namespace ecgpu {
+
+struct FusedOp {
+  std::vector<void*> srcs;     // buffers whose ORIGINAL contents are read
+  std::vector<void*> dsts;     // buffers written (final contents)
+  std::vector<uint8_t> coef;   // dsts.size() x srcs.size(), row-major
+  // Reference byte counters (jerasure.cpp:42-44): xor, gf-multiply, memcpy.
+  double xor_bytes = 0, gf_bytes = 0, memcpy_bytes = 0;
+  bool dst_is_src = false;     // some output buffer is also read
+};
+
+class LinearTracker {
+ public:
+  // Registers (or finds) a buffer; identity is the pointer value.
+  int id(void* p);
+
+  // Whole-region primitives (GF(2^8)).
+  void copy(void* dst, void* src);                 // dst = src
+  void xor3(void* r1, void* r2, void* r3);         // r3 = r1 ^ r2
+  void mul(void* src, int c, void* dst, bool add);  // dst (^)= c * src
+
+  // jerasure_matrix_dotprod semantics (jerasure.cpp:561-620), w = 8, with
+  // its stats accounting.  size only feeds the byte counters.
+  void dotprod(int k, const int* row, const int* src_ids, int dest_id, char** data, char** coding, int64_t size);
+
+  // Adds to the byte counters like jerasure_do_parity etc. do.
+  void count(double xor_b, double gf_b, double memcpy_b) {
+    xor_ += xor_b;
+    gf_ += gf_b;
+    memcpy_ += memcpy_b;
+  }
+
+  FusedOp finish() const;
+
+ private:
+  using Vec = std::vector<uint8_t>;
+  Vec& state(int b);
+  std::vector<void*> bufs_;
+  std::unordered_map<void*, int> idx_;
+  std::vector<Vec> state_;
+  std::vector<char> written_;
+  double xor_ = 0, gf_ = 0, memcpy_ = 0;
+};
+
+// jerasure_matrix_encode (jerasure.cpp:285-299) as a fused op, w = 8.
+void plan_encode(LinearTracker& t, int k, int m, const int* matrix, char** data, char** coding, int64_t size);
+
+// jerasure_matrix_decode (jerasure.cpp:153-254) as a fused op, w = 8.
+// Returns 0, or -1 where the reference returns -1 (too many erasures,
+// singular survivor matrix); nothing is recorded in that case.
+int plan_decode(LinearTracker& t, int k, int m, const int* matrix, int row_k_ones, const int* erasures, char** data,
+                char** coding, int64_t size);
+
+}  // namespace ecgpu

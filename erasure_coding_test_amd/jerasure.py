@@ -1,0 +1,108 @@
+"""jerasure.h surface (reference include/jerasure.h:113-282) over the C ABI.
+
+Same names, argument order and meaning as the reference:
+``data_ptrs`` / ``coding_ptrs`` are sequences of k / m shard buffers (CUDA
+tensors are used in place; CPU tensors or numpy arrays are staged through
+HBM), ``matrix`` is the flat row-major m x k coding matrix, ``erasures`` the
+erased ids (a trailing -1 is optional).  Encode/decode/dotprod run on the
+MI355X and are synchronous; a HIP failure raises ``EcgpuError`` (there is no
+CPU fallback).  Where the reference calls exit(1) (bad w) this raises
+ValueError; where it returns -1 this returns -1.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+from . import _native as N
+from ._buffers import addr, addrs
+
+
+def _erasure_list(erasures: Sequence[int]) -> list:
+    er = [int(e) for e in erasures]
+    if not er or er[-1] != -1:
+        er.append(-1)
+    return er
+
+
+def jerasure_matrix_encode(k: int, m: int, w: int, matrix, data_ptrs, coding_ptrs, size: int) -> None:
+    if w != 8:
+        raise ValueError("jerasure_matrix_encode: the MI355X path implements w = 8")
+    rc = N.lib.ecgpu_jerasure_matrix_encode(k, m, w, N.int_array(matrix), N.ptr_array(addrs(data_ptrs)),
+                                            N.ptr_array(addrs(coding_ptrs)), size)
+    N.check(rc, "jerasure_matrix_encode")
+
+
+def jerasure_matrix_decode(k: int, m: int, w: int, matrix, row_k_ones: int, erasures, data_ptrs, coding_ptrs,
+                           size: int) -> int:
+    if w != 8:
+        raise ValueError("jerasure_matrix_decode: the MI355X path implements w = 8")
+    rc = N.lib.ecgpu_jerasure_matrix_decode(k, m, w, N.int_array(matrix), row_k_ones,
+                                            N.int_array(_erasure_list(erasures)), N.ptr_array(addrs(data_ptrs)),
+                                            N.ptr_array(addrs(coding_ptrs)), size)
+    return N.check(rc, "jerasure_matrix_decode")
+
+
+def jerasure_matrix_dotprod(k: int, w: int, matrix_row, src_ids: Optional[Sequence[int]], dest_id: int, data_ptrs,
+                            coding_ptrs, size: int) -> None:
+    if w != 8:
+        raise ValueError("jerasure_matrix_dotprod: the MI355X path implements w = 8")
+    ids = None if src_ids is None else N.int_array(src_ids)
+    rc = N.lib.ecgpu_jerasure_matrix_dotprod(k, w, N.int_array(matrix_row), ids, dest_id,
+                                             N.ptr_array(addrs(data_ptrs)), N.ptr_array(addrs(coding_ptrs)), size)
+    N.check(rc, "jerasure_matrix_dotprod")
+
+
+def jerasure_do_parity(k: int, data_ptrs, parity_ptr, size: int) -> None:
+    N.check(N.lib.ecgpu_jerasure_do_parity(k, N.ptr_array(addrs(data_ptrs)), addr(parity_ptr), size),
+            "jerasure_do_parity")
+
+
+def jerasure_make_decoding_matrix(k: int, m: int, w: int, matrix, erased) -> Tuple[int, List[int], List[int]]:
+    dm, ids = (N.c_int * (k * k))(), (N.c_int * k)()
+    rc = N.lib.ecgpu_jerasure_make_decoding_matrix(k, m, w, N.int_array(matrix), N.int_array(erased), dm, ids)
+    return rc, list(dm), list(ids)
+
+
+def jerasure_invert_matrix(mat, rows: int, w: int) -> Tuple[int, List[int], List[int]]:
+    """Returns (rc, inverse, mat-after) -- the reference destroys mat in place."""
+    a, inv = N.int_array(mat), (N.c_int * (rows * rows))()
+    rc = N.lib.ecgpu_jerasure_invert_matrix(a, inv, rows, w)
+    return rc, list(inv), list(a)[: rows * rows]
+
+
+def jerasure_invertible_matrix(mat, rows: int, w: int) -> int:
+    return N.lib.ecgpu_jerasure_invertible_matrix(N.int_array(mat), rows, w)
+
+
+def jerasure_erasures_to_erased(k: int, m: int, erasures) -> Optional[List[int]]:
+    return N.take_int_matrix(N.lib.ecgpu_jerasure_erasures_to_erased(k, m, N.int_array(_erasure_list(erasures))),
+                             k + m)
+
+
+def jerasure_matrix_multiply(m1, m2, r1: int, c1: int, r2: int, c2: int, w: int) -> List[int]:
+    return N.take_int_matrix(N.lib.ecgpu_jerasure_matrix_multiply(N.int_array(m1), N.int_array(m2), r1, c1, r2, c2,
+                                                                  w), r1 * c2)
+
+
+def jerasure_get_stats() -> List[float]:
+    """[bytes XORed, bytes GF-multiplied, bytes copied] since the last call (jerasure.cpp:1143-1151 order)."""
+    out = (N.ctypes.c_double * 3)()
+    N.lib.ecgpu_jerasure_get_stats(out)
+    return list(out)
+
+
+def decode_plan(k: int, m: int, matrix, erasures, row_k_ones: int = 0):
+    """The single fused linear map jerasure_matrix_decode applies: returns
+    (out_ids, src_ids, coefs[n_out][n_src]) over shard ids, or None where the
+    reference decode returns -1."""
+    n = k + m
+    out_ids, src_ids = (N.c_int * n)(), (N.c_int * n)()
+    n_out, n_src = N.c_int(0), N.c_int(0)
+    coefs = (N.c_int * (n * n))()
+    rc = N.lib.ecgpu_decode_plan(k, m, 8, N.int_array(matrix), row_k_ones, N.int_array(_erasure_list(erasures)),
+                                 out_ids, N.ctypes.byref(n_out), src_ids, N.ctypes.byref(n_src), coefs)
+    if rc == N.ECGPU_ERR:
+        return None
+    N.check(rc, "ecgpu_decode_plan")
+    no, ns = n_out.value, n_src.value
+    return (list(out_ids)[:no], list(src_ids)[:ns], [list(coefs[r * ns:(r + 1) * ns]) for r in range(no)])

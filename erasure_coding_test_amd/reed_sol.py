@@ -1,0 +1,39 @@
+"""reed_sol.h surface (reference include/reed_sol.h:33-42) over the C ABI.
+
+Matrices come back as flat row-major Python int lists (m*k entries), or None
+where the reference returns NULL.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+from . import _native as N
+from ._buffers import addrs
+
+
+def reed_sol_vandermonde_coding_matrix(k: int, m: int, w: int) -> Optional[List[int]]:
+    return N.take_int_matrix(N.lib.ecgpu_reed_sol_vandermonde_coding_matrix(k, m, w), k * m)
+
+
+def reed_sol_extended_vandermonde_matrix(rows: int, cols: int, w: int) -> Optional[List[int]]:
+    return N.take_int_matrix(N.lib.ecgpu_reed_sol_extended_vandermonde_matrix(rows, cols, w), rows * cols)
+
+
+def reed_sol_big_vandermonde_distribution_matrix(rows: int, cols: int, w: int) -> Optional[List[int]]:
+    return N.take_int_matrix(N.lib.ecgpu_reed_sol_big_vandermonde_distribution_matrix(rows, cols, w), rows * cols)
+
+
+def reed_sol_r6_coding_matrix(k: int, w: int) -> Optional[List[int]]:
+    return N.take_int_matrix(N.lib.ecgpu_reed_sol_r6_coding_matrix(k, w), 2 * k)
+
+
+def reed_sol_r6_encode(k: int, w: int, data_ptrs, coding_ptrs, size: int) -> int:
+    """RAID-6 P/Q encode (reed_sol.cpp:200-225); w must be 8 here."""
+    return N.check(N.lib.ecgpu_reed_sol_r6_encode(k, w, N.ptr_array(addrs(data_ptrs)),
+                                                  N.ptr_array(addrs(coding_ptrs)), size), "reed_sol_r6_encode")
+
+
+def reed_sol_galois_w08_region_multby_2(region, nbytes: int) -> None:
+    from ._buffers import addr
+    N.check(N.lib.ecgpu_reed_sol_galois_w08_region_multby_2(addr(region), nbytes),
+            "reed_sol_galois_w08_region_multby_2")

@@ -1,0 +1,130 @@
+/*
+ * ecgpu.h -- C ABI of the MI355X (gfx950) Reed-Solomon GF(2^8) coding library.
+ *
+ * The drop-in boundary of this repo.  Every entry point is extern "C", takes
+ * plain pointers and sizes, and replaces one function of the reference's
+ * coding surface (canghaiyang/Erasure_Coding_Test, vendored Jerasure 1.2:
+ * include/galois.h, include/jerasure.h, include/reed_sol.h).  The cited
+ * file:line is the reference function each entry point replaces; argument
+ * meaning, ownership (malloc'd results freed with free()) and return
+ * conventions are the reference's.  libjerasure_amd.so re-exports the same
+ * functions under the reference's own (C++-mangled) names, so callers built
+ * against the reference headers link unchanged.
+ *
+ * Hot path (GPU): ecgpu_jerasure_matrix_encode / _decode / _dotprod,
+ * ecgpu_galois_w08_region_multiply, ecgpu_galois_region_xor,
+ * ecgpu_jerasure_do_parity, ecgpu_reed_sol_r6_encode (w=8) and the batched
+ * device-resident plan API below.  These accept host OR device pointers
+ * (classified per buffer; host buffers are staged through HBM) and are
+ * synchronous: results are valid on return, like the reference.  They never
+ * fall back to a CPU path; a HIP failure returns ECGPU_ERR_HIP (or, through
+ * the void-returning drop-in names, aborts with a message).
+ *
+ * Host-only (no GPU touched): field arithmetic, matrix construction,
+ * inversion and decode planning.
+ */
+#ifndef ECGPU_H
+#define ECGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define ECGPU_API __attribute__((visibility("default")))
+#else
+#define ECGPU_API
+#endif
+
+enum {
+  ECGPU_OK = 0,
+  ECGPU_ERR = -1,         /* reference-style failure (e.g. too many erasures) */
+  ECGPU_ERR_ARG = -2,     /* invalid argument (w, k, m, size, pointers)       */
+  ECGPU_ERR_HIP = -3,     /* HIP runtime / kernel launch failure              */
+  ECGPU_ERR_NOMEM = -4
+};
+
+enum { ECGPU_KERNEL_PERM = 0, ECGPU_KERNEL_LDS = 1 };
+
+/* ---------------------------------------------------------------- misc -- */
+ECGPU_API const char* ecgpu_version(void);
+ECGPU_API const char* ecgpu_last_error(void);         /* thread-local message */
+ECGPU_API void ecgpu_free(void* p);                    /* == free()           */
+
+/* ------------------------------------- GF(2^w) scalar ops (host only) --- */
+ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w); /* galois.cpp:322-360 */
+ECGPU_API int ecgpu_galois_single_divide(int a, int b, int w);   /* galois.cpp:367-398 */
+ECGPU_API int ecgpu_galois_inverse(int a, int w);                /* galois.cpp:597-603 */
+ECGPU_API int ecgpu_galois_log(int value, int w);                /* galois.cpp:280-289 */
+ECGPU_API int ecgpu_galois_ilog(int value, int w);               /* galois.cpp:269-278 */
+
+/* ------------------------------------------- matrices (host only) ------- */
+ECGPU_API int* ecgpu_reed_sol_vandermonde_coding_matrix(int k, int m, int w);            /* reed_sol.cpp:63-84   */
+ECGPU_API int* ecgpu_reed_sol_extended_vandermonde_matrix(int rows, int cols, int w);    /* reed_sol.cpp:227-255 */
+ECGPU_API int* ecgpu_reed_sol_big_vandermonde_distribution_matrix(int rows, int cols, int w); /* reed_sol.cpp:257-352 */
+ECGPU_API int* ecgpu_reed_sol_r6_coding_matrix(int k, int w);                            /* reed_sol.cpp:43-61   */
+ECGPU_API int ecgpu_jerasure_invert_matrix(int* mat, int* inv, int rows, int w);         /* jerasure.cpp:360-445 */
+ECGPU_API int ecgpu_jerasure_invertible_matrix(int* mat, int rows, int w);               /* jerasure.cpp:447-502 */
+ECGPU_API int* ecgpu_jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, int r2, int c2, int w); /* jerasure.cpp:1126-1141 */
+ECGPU_API int* ecgpu_jerasure_erasures_to_erased(int k, int m, int* erasures);           /* jerasure.cpp:507-532 */
+ECGPU_API int ecgpu_jerasure_make_decoding_matrix(int k, int m, int w, int* matrix, int* erased,
+                                                  int* decoding_matrix, int* dm_ids);    /* jerasure.cpp:84-112  */
+
+/* Fused decode plan (host only): the single linear map that
+ * jerasure_matrix_decode (jerasure.cpp:153-254) applies, over shard ids
+ * 0..k+m-1.  On return out_ids[0..*n_out) are the shard ids written,
+ * src_ids[0..*n_src) the shard ids read, coefs row-major n_out x n_src.
+ * Arrays must hold k+m (ids) and (k+m)^2 (coefs) entries.  Returns 0 or -1
+ * exactly where the reference decode returns -1.  w must be 8. */
+ECGPU_API int ecgpu_decode_plan(int k, int m, int w, const int* matrix, int row_k_ones, const int* erasures,
+                                int* out_ids, int* n_out, int* src_ids, int* n_src, int* coefs);
+
+/* ------------------------------------ hot path: reference semantics ----- */
+/* jerasure.cpp:285-299.  w must be 8 (w=16/32 live in the drop-in library). */
+ECGPU_API int ecgpu_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs,
+                                           int size);
+/* jerasure.cpp:153-254.  Returns 0 / -1 like the reference. */
+ECGPU_API int ecgpu_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures,
+                                           char** data_ptrs, char** coding_ptrs, int size);
+/* jerasure.cpp:561-620 */
+ECGPU_API int ecgpu_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int dest_id,
+                                            char** data_ptrs, char** coding_ptrs, int size);
+/* jerasure.cpp:347-358 */
+ECGPU_API int ecgpu_jerasure_do_parity(int k, char** data_ptrs, char* parity_ptr, int size);
+/* galois.cpp:415-467 */
+ECGPU_API int ecgpu_galois_w08_region_multiply(char* region, int multby, int nbytes, char* r2, int add);
+/* galois.cpp:731-754 */
+ECGPU_API int ecgpu_galois_region_xor(char* r1, char* r2, char* r3, int nbytes);
+/* reed_sol.cpp:200-225 (w = 8) and reed_sol.cpp:112-152 */
+ECGPU_API int ecgpu_reed_sol_r6_encode(int k, int w, char** data_ptrs, char** coding_ptrs, int size);
+ECGPU_API int ecgpu_reed_sol_galois_w08_region_multby_2(char* region, int nbytes);
+/* jerasure.cpp:1143-1151: fills xor, gf, memcpy byte counts and resets. */
+ECGPU_API int ecgpu_jerasure_get_stats(double* fill_in);
+
+/* ---------------------- hot path: batched, device-resident, async ------- */
+/* A plan = one rows x nsrc GF(2^8) coefficient matrix (uploaded once) bound
+ * to a table of device pointers for `stripes` stripes:
+ *     dst[s][r] = XOR_j coefs[r][j] * src[s][j]   over `size` bytes.
+ * Launches are asynchronous on the given hipStream_t (NULL = default stream)
+ * and graph-capturable once bound.  SURVEY.md §8b "batched device API". */
+typedef struct ecgpu_plan ecgpu_plan;
+ECGPU_API ecgpu_plan* ecgpu_plan_create(int rows, int nsrc, const int* coefs, int device);
+ECGPU_API int ecgpu_plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src_ptrs, uint8_t* const* dst_ptrs,
+                              int64_t size);
+ECGPU_API int ecgpu_plan_set_kernel(ecgpu_plan* p, int kind, int nontemporal);
+ECGPU_API int ecgpu_plan_launch(ecgpu_plan* p, void* stream);
+ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p);
+
+/* Convenience: encode `stripes` device-resident stripes with the m x k
+ * coding matrix (pointer tables are host arrays of device pointers, stripe-
+ * major: data[s*k + j], coding[s*m + i]).  Asynchronous on `stream`. */
+ECGPU_API int ecgpu_encode_batch(int k, int m, const int* matrix, int stripes, const uint8_t* const* data,
+                                 uint8_t* const* coding, int64_t size, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ECGPU_H */

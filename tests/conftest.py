@@ -1,0 +1,54 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TESTS = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, TESTS):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN_DIR = os.path.join(TESTS, "golden")
+REFERENCE_ROOT = "/root/reference"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box with -m gpu)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(GOLDEN_DIR, "golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def vectors():
+    with np.load(os.path.join(GOLDEN_DIR, "vectors.npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
+def restatement():
+    from oracle.oracle import Restatement
+    return Restatement()
+
+
+@pytest.fixture(scope="session")
+def reference():
+    from oracle.oracle import Reference
+    try:
+        return Reference()
+    except (FileNotFoundError, OSError):
+        pytest.skip("oracle/_ref not built (needs /root/reference at build time)")
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X (run with -m gpu on the GPU box)"
+    import erasure_coding_test_amd  # noqa: F401
+    return torch.device("cuda:0")

@@ -1,0 +1,359 @@
+"""GPU parity: the MI355X path (through the C ABI, include/ecgpu.h) against the
+golden vectors made by the reference and against the CPU oracle.
+
+Bit-exact everywhere (integer/byte work).  Small sizes compare bytes; full
+BASELINE sizes compare FNV-1a digests pinned by the reference plus
+size-independent properties (encode -> erase -> decode round trips).
+"""
+import ctypes
+import itertools
+import os
+import random
+
+import numpy as np
+import pytest
+
+from ecdata import CONFIGS, fnv1a64, shard_seed, splitmix_bytes
+from oracle.oracle import alloc_shards
+
+pytestmark = pytest.mark.gpu
+
+PAD = 16
+
+
+def host_shards(cfg, stripe, count, size, first=0):
+    out = alloc_shards(count, size, PAD)
+    for s in range(count):
+        out[s][:size] = splitmix_bytes(size, shard_seed(cfg, stripe, first + s))
+    return out
+
+
+def to_dev(arrs, dev):
+    import torch
+    return [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in arrs]
+
+
+def to_host(tensors):
+    return [t.cpu().numpy() for t in tensors]
+
+
+def digests(bufs, size):
+    return [fnv1a64(np.asarray(b)[:size]) for b in bufs]
+
+
+@pytest.fixture(scope="module")
+def ec(gpu):
+    import erasure_coding_test_amd as E
+    return E
+
+
+# ------------------------------------------------------------ golden ----
+@pytest.mark.parametrize("where", ["device", "host"])
+@pytest.mark.parametrize("cfg", sorted(CONFIGS))
+def test_encode_small_golden(ec, gpu, golden, vectors, cfg, where):
+    k, m = CONFIGS[cfg]["k"], CONFIGS[cfg]["m"]
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    for size in (4096, 4099, 1000, 7, 1):
+        for stripe in range(2):
+            data = host_shards(cfg, stripe, k, size)
+            coding = alloc_shards(m, size, PAD)
+            if where == "device":
+                dd, dc = to_dev(data, gpu), to_dev(coding, gpu)
+                ec.jerasure.jerasure_matrix_encode(k, m, 8, M, dd, dc, size)
+                coding = to_host(dc)
+            else:
+                ec.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, size)
+            assert digests(coding, size) == golden["encode_small"][f"C{cfg}:{size}:{stripe}"], (size, stripe)
+            if size == 4096:
+                assert np.array_equal(np.stack([c[:size] for c in coding]), vectors[f"enc_{cfg}_{stripe}"])
+
+
+def test_decode_inconsistent_golden(ec, gpu, golden):
+    mats = {}
+    for case in golden["decode_inconsistent"]:
+        k, m, cfg, size = case["k"], case["m"], case["cfg"], case["size"]
+        if (k, m) not in mats:
+            mats[(k, m)] = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+        bufs = to_dev(host_shards(cfg, 7, k, size) + host_shards(cfg, 7, m, size, first=k), gpu)
+        rc = ec.jerasure.jerasure_matrix_decode(k, m, 8, mats[(k, m)], case["row_k_ones"], case["erasures"],
+                                                bufs[:k], bufs[k:], size)
+        assert rc == case["rc"], case["erasures"]
+        assert digests(to_host(bufs), size) == case["digests"], (case["erasures"], case["row_k_ones"])
+
+
+def test_dotprod_golden(ec, gpu, golden):
+    for t, case in enumerate(golden["dotprod"]):
+        k, m, size = case["k"], case["m"], case["size"]
+        bufs = to_dev(host_shards(9, case["seed_stripe"], k, size) +
+                      host_shards(9, case["seed_stripe"], m, size, first=k), gpu)
+        ec.jerasure.jerasure_matrix_dotprod(k, 8, case["row"], case["src_ids"], case["dest_id"], bufs[:k], bufs[k:],
+                                            size)
+        assert digests(to_host(bufs), size) == case["digests"], t
+
+
+def test_region_ops_golden(ec, gpu, golden):
+    for case in golden["region_multiply"]:
+        size, t = case["size"], case["seed_stripe"]
+        src, dst = to_dev([host_shards(10, t, 1, size)[0], host_shards(10, t, 1, size, first=1)[0]], gpu)
+        if case["mode"] == "r2":
+            ec.galois.galois_w08_region_multiply(src, case["multby"], size, dst, case["add"])
+            out = dst
+        else:
+            ec.galois.galois_w08_region_multiply(src, case["multby"], size, None, case["add"])
+            out = src
+        assert fnv1a64(out.cpu().numpy()[:size]) == case["digest"], case
+    for case in golden["region_xor"]:
+        size = case["size"]
+        a, b, c = to_dev(host_shards(11, case["seed_stripe"], 2, size) + alloc_shards(1, size, PAD), gpu)
+        ec.galois.galois_region_xor(a, b, c, size)
+        assert fnv1a64(c.cpu().numpy()[:size]) == case["digest"]
+        ec.galois.galois_region_xor(a, b, a, size)  # r3 aliasing r1
+        assert fnv1a64(a.cpu().numpy()[:size]) == case["digest"]
+
+
+def test_stats_semantics(ec, gpu, golden):
+    k, m = 10, 4
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    ec.jerasure.jerasure_get_stats()
+    data = to_dev(host_shards(3, 0, k, 4096), gpu)
+    coding = to_dev(alloc_shards(m, 4096, PAD), gpu)
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, 4096)
+    assert ec.jerasure.jerasure_get_stats() == golden["stats_after_rs10_4_encode_4096"]
+    ec.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, [0, 1, 2, 3], data, coding, 4096)
+    assert ec.jerasure.jerasure_get_stats() == golden["stats_after_rs10_4_decode_0123_4096"]
+
+
+# ---------------------------------------------------- full BASELINE sizes ----
+@pytest.mark.parametrize("name", ["C2", "C3", "C5"])
+def test_full_size_digests(ec, gpu, golden, name):
+    import torch
+    g = golden["full_size"][name]
+    cfg = int(name[1:])
+    k, m, size = g["k"], g["m"], g["size"]
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = [splitmix_bytes(size, shard_seed(cfg, 0, s)) for s in range(k)]
+    assert [fnv1a64(d) for d in data] == g["data"]
+    dd = to_dev(data, gpu)
+    dc = [torch.empty(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, dd, dc, size)
+    assert [fnv1a64(c.cpu().numpy()) for c in dc] == g["coding"]
+
+
+@pytest.mark.parametrize("erasures", [[0], [5], [10], [0, 1, 2, 3], [3, 7, 11, 13], [9, 10, 11, 12], [0, 13]])
+def test_full_size_roundtrip_rs10_4(ec, gpu, erasures):
+    import torch
+    k, m, size = 10, 4, 4 << 20
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    g = torch.Generator(device="cpu").manual_seed(sum(erasures) + 17)
+    data = [torch.randint(0, 256, (size,), dtype=torch.uint8, generator=g).to(gpu) for _ in range(k)]
+    coding = [torch.empty(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, size)
+    orig = [t.clone() for t in data + coding]
+    bufs = [t.clone() for t in orig]
+    for e in erasures:
+        bufs[e].fill_(0x5A)
+    assert ec.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, erasures, bufs[:k], bufs[k:], size) == 0
+    for a, b in zip(bufs, orig):
+        assert torch.equal(a, b)
+
+
+def test_too_many_erasures_returns_minus_one(ec, gpu):
+    k, m, size = 6, 3, 64
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    bufs = to_dev(host_shards(2, 0, k + m, size), gpu)
+    before = to_host(bufs)
+    assert ec.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, [0, 1, 2, 3], bufs[:k], bufs[k:], size) == -1
+    for a, b in zip(to_host(bufs), before):
+        assert np.array_equal(a, b)
+
+
+# ----------------------------------------------------- batched plan API ----
+def _encode_ref(restatement, k, m, M, data, size):
+    coding = alloc_shards(m, size, PAD)
+    restatement.matrix_encode(k, m, np.array(M).reshape(m, k), data, coding, size)
+    return coding
+
+
+@pytest.mark.parametrize("kind,nt", [(0, 1), (0, 0), (1, 1), (1, 0)])
+@pytest.mark.parametrize("k,m", [(4, 2), (6, 3), (10, 4), (12, 4), (16, 3), (1, 1), (3, 4)])
+def test_plan_batch_kernels(ec, gpu, restatement, kind, nt, k, m):
+    import torch
+    size, stripes = 65536 + 48, 5
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8) if k > 1 else [7] * m
+    hdata = [host_shards(20 + k, s, k, size) for s in range(stripes)]
+    data = [to_dev(h, gpu) for h in hdata]
+    coding = [[torch.zeros(size + PAD, dtype=torch.uint8, device=gpu) for _ in range(m)] for _ in range(stripes)]
+    p = ec.plan.encode_plan(k, m, M).bind(data, coding, size).set_kernel(kind, bool(nt))
+    p.launch()
+    torch.cuda.synchronize()
+    for s in range(stripes):
+        ref = _encode_ref(restatement, k, m, M, hdata[s], size)
+        for a, b in zip(to_host(coding[s]), ref):
+            assert np.array_equal(a[:size], b[:size]), (s,)
+            assert not a[size:].any()  # nothing written past the shard
+
+
+@pytest.mark.parametrize("k,m", [(17, 2), (20, 4), (32, 3), (24, 6)])
+def test_generic_k_and_many_rows(ec, gpu, restatement, k, m):
+    size = 40000 + 5
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    hdata = host_shards(30, k, k, size)
+    dd, dc = to_dev(hdata, gpu), to_dev(alloc_shards(m, size, PAD), gpu)
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, dd, dc, size)
+    for a, b in zip(to_host(dc), _encode_ref(restatement, k, m, M, hdata, size)):
+        assert np.array_equal(a[:size], b[:size])
+
+
+@pytest.mark.parametrize("offset", [1, 3, 8, 15])
+def test_misaligned_buffers(ec, gpu, restatement, offset):
+    import torch
+    k, m, size = 6, 3, 10007
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    hdata = host_shards(31, offset, k, size)
+    base = [torch.zeros(size + 64, dtype=torch.uint8, device=gpu) for _ in range(k + m)]
+    views = [b[offset:offset + size] for b in base]
+    for v, h in zip(views[:k], hdata):
+        v.copy_(torch.from_numpy(h[:size]))
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, views[:k], views[k:], size)
+    for a, b in zip(views[k:], _encode_ref(restatement, k, m, M, hdata, size)):
+        assert np.array_equal(a.cpu().numpy(), b[:size])
+
+
+def test_aliased_coding_buffers_follow_sequential_semantics(ec, gpu, restatement):
+    # coding[0] aliases data[2]: the reference overwrites data[2] with parity 0
+    # before computing parity 1..; the fused plan must reproduce that exactly.
+    k, m, size = 6, 6, 5000
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    hdata = host_shards(32, 0, k, size)
+    hcoding = alloc_shards(m, size, PAD)
+    hcoding[0] = hdata[2]
+    restatement.matrix_encode(k, m, np.array(M).reshape(m, k), hdata, hcoding, size)
+    ref = [x.copy() for x in hdata + hcoding[1:]]
+    dd = to_dev(host_shards(32, 0, k, size), gpu)
+    dc = [dd[2]] + to_dev(alloc_shards(m - 1, size, PAD), gpu)
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, dd, dc, size)
+    for a, b in zip(to_host(dd + dc[1:]), ref):
+        assert np.array_equal(a[:size], b[:size])
+
+
+def test_decode_plan_batch_matches_jerasure(ec, gpu):
+    import torch
+    k, m, size, stripes = 10, 4, 1 << 18, 4
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    shards = []
+    for _ in range(stripes):
+        d = [torch.randint(0, 256, (size,), dtype=torch.uint8, generator=g).to(gpu) for _ in range(k)]
+        c = [torch.empty(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+        ec.jerasure.jerasure_matrix_encode(k, m, 8, M, d, c, size)
+        shards.append(d + c)
+    orig = [[t.clone() for t in st] for st in shards]
+    for er in ([0], [0, 1, 2, 3], [2, 11], [10, 11, 12, 13]):
+        for st in shards:
+            for e in er:
+                st[e].zero_()
+        dp = ec.plan.DecodePlan(k, m, M, er)
+        dp.bind_stripes(shards, size).launch()
+        torch.cuda.synchronize()
+        for st, o in zip(shards, orig):
+            for a, b in zip(st, o):
+                assert torch.equal(a, b), er
+
+
+# --------------------------------------------------- other hot-path ops ----
+def test_r6_and_parity(ec, gpu, restatement):
+    k, size = 8, 9999
+    hdata = host_shards(33, 0, k, size)
+    dd, dc = to_dev(hdata, gpu), to_dev(alloc_shards(2, size, PAD), gpu)
+    assert ec.reed_sol.reed_sol_r6_encode(k, 8, dd, dc, size) == 1
+    R6 = ec.reed_sol.reed_sol_r6_coding_matrix(k, 8)
+    ref = _encode_ref(restatement, k, 2, R6, hdata, size)
+    for a, b in zip(to_host(dc), ref):
+        assert np.array_equal(a[:size], b[:size])
+    par = to_dev(alloc_shards(1, size, PAD), gpu)[0]
+    ec.jerasure.jerasure_do_parity(k, dd, par, size)
+    x = np.zeros(size, np.uint8)
+    for h in hdata:
+        x ^= h[:size]
+    assert np.array_equal(par.cpu().numpy()[:size], x)
+    t = dd[0].clone()
+    ec.reed_sol.reed_sol_galois_w08_region_multby_2(t, size)
+    ref2 = hdata[0].copy()
+    restatement.region_multiply(ref2, 2, size, None, 0)
+    assert np.array_equal(t.cpu().numpy()[:size], ref2[:size])
+
+
+# --------------------------------------------- the C++ drop-in library ----
+def _dropin():
+    from erasure_coding_test_amd._native import DROPIN_PATH
+    L = ctypes.CDLL(DROPIN_PATH)
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    i = ctypes.c_int
+    enc = L._Z22jerasure_matrix_encodeiiiPiPPcS1_i
+    enc.argtypes, enc.restype = [i, i, i, ctypes.POINTER(i), pp, pp, i], None
+    vdm = L._Z34reed_sol_vandermonde_coding_matrixiii
+    vdm.argtypes, vdm.restype = [i, i, i], ctypes.c_void_p
+    rmul = L._Z26galois_w08_region_multiplyPciiS_i
+    rmul.argtypes, rmul.restype = [ctypes.c_void_p, i, i, ctypes.c_void_p, i], None
+    rxor = L._Z17galois_region_xorPcS_S_i
+    rxor.argtypes, rxor.restype = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, i], None
+    return L, enc, vdm, rmul, rxor
+
+
+def test_dropin_cpp_encode_host_buffers(gpu, restatement):
+    L, enc, vdm, _, _ = _dropin()
+    k, m, size = 3, 3, (1 << 20) + 5  # the reference client's EC_K/EC_M (ych_ec_test.h:5-6)
+    mp = vdm(k, m, 8)
+    M = list((ctypes.c_int * (k * m)).from_address(mp))
+    hdata = host_shards(34, 0, k, size)
+    coding = alloc_shards(m, size, PAD)
+    arr = lambda bufs: (ctypes.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+    enc(k, m, 8, (ctypes.c_int * (k * m))(*M), arr(hdata), arr(coding), size)
+    for a, b in zip(coding, _encode_ref(restatement, k, m, M, hdata, size)):
+        assert np.array_equal(a[:size], b[:size])
+
+
+def test_dropin_ecx_incremental_accumulate(gpu, restatement):
+    # ecx_datanode_main.cpp:680-735: blocks of a 1 MiB chunk split in 3
+    # (349,525 B -- not a multiple of 8) arrive one source at a time; each
+    # parity accumulator is memcpy'd / XORed / multiply-added with init[].
+    L, _, vdm, rmul, rxor = _dropin()
+    k, m, bs = 3, 3, (1 << 20) // 3
+    M = list((ctypes.c_int * (k * m)).from_address(vdm(k, m, 8)))
+    blocks = host_shards(35, 0, k, bs)
+    acc = alloc_shards(m, bs, 8)
+    init = [0] * m
+    for j in range(k):
+        for i in range(m):
+            c = M[i * k + j]
+            if c == 1:
+                if not init[i]:
+                    acc[i][:bs] = blocks[j][:bs]
+                    init[i] = 1
+                else:
+                    rxor(blocks[j].ctypes.data, acc[i].ctypes.data, acc[i].ctypes.data, bs)
+            elif c != 0:
+                rmul(blocks[j].ctypes.data, c, bs, acc[i].ctypes.data, init[i])
+                init[i] = 1
+    for a, b in zip(acc, _encode_ref(restatement, k, m, M, blocks, bs)):
+        assert np.array_equal(a[:bs], b[:bs])
+
+
+def test_all_erasure_patterns_rs63_device(ec, gpu):
+    import torch
+    k, m, size = 6, 3, 4096 + 7
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = to_dev(host_shards(2, 9, k, size), gpu)
+    coding = [torch.empty(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, size)
+    orig = [t[:size].clone() for t in data] + [t.clone() for t in coding]
+    for e in range(1, m + 1):
+        for er in itertools.combinations(range(k + m), e):
+            bufs = [t.clone() for t in orig]
+            for i in er:
+                bufs[i].fill_(0xEE)
+            for rko in (0, 1):
+                b2 = [t.clone() for t in bufs]
+                assert ec.jerasure.jerasure_matrix_decode(k, m, 8, M, rko, list(er), b2[:k], b2[k:], size) == 0
+                for a, b in zip(b2, orig):
+                    assert torch.equal(a, b), (er, rko)

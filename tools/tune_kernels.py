@@ -1,0 +1,113 @@
+"""A/B the gf_apply kernel variants on the MI355X in ONE process (interleaved
+rounds, median of each), against a streaming-copy reference with the same
+byte volume.  Workload = the bench's: RS(10,4), 4 MiB shards, 24 stripes.
+
+    python tools/tune_kernels.py [--rounds 15] [--stripes 24]
+
+Prints one JSON object per variant: median/min launch ms and GB/s of
+algorithmic HBM traffic ((K+R) * S per stripe; copy: 2 * S per pair).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import erasure_coding_test_amd as E  # noqa: E402
+from erasure_coding_test_amd import _native as N  # noqa: E402
+
+L = ctypes.CDLL(os.path.join(N.LIB_DIR, "libecgpu_diag.so"))
+L.ecgpu_diag_launch.restype = ctypes.c_int
+L.ecgpu_diag_launch.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p] * 4 + [
+    ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_void_p]
+
+
+def tables(coefs):
+    gm = E.galois.galois_single_multiply
+    q, nib = [], []
+    for c in coefs:
+        for p in range(4):
+            q.append(sum(gm(c, e << (2 * p), 8) << (8 * e) for e in range(4)))
+        nib += [gm(c, x, 8) for x in range(16)] + [gm(c, x << 4, 8) for x in range(16)]
+    return (torch.tensor(q, dtype=torch.int64).to(torch.int32).cuda(),
+            torch.tensor(nib, dtype=torch.uint8).cuda())
+
+
+def masks(coefs):
+    unit = sum(1 << i for i, c in enumerate(coefs) if c == 1)
+    zero = sum(1 << i for i, c in enumerate(coefs) if c == 0)
+    return unit, zero
+
+
+def ptr_table(ptrs):
+    return torch.tensor(ptrs, dtype=torch.int64).cuda()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=15)
+    ap.add_argument("--stripes", type=int, default=24)
+    args = ap.parse_args()
+    k, m, S, B = 10, 4, 4 << 20, args.stripes
+    slab = torch.empty((B, k + m, S), dtype=torch.uint8, device="cuda")
+    slab.random_(0, 256, generator=torch.Generator(device="cuda").manual_seed(5))
+    addr = lambda s, i: slab[s, i].data_ptr()
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    q_enc, n_enc = tables(M)
+    u_enc, z_enc = masks(M)
+    src_enc = ptr_table([addr(s, j) for s in range(B) for j in range(k)])
+    dst_enc = ptr_table([addr(s, k + i) for s in range(B) for i in range(m)])
+    dec_rows = {"ones": [1] * k, "dense": [150, 119, 240, 20, 249, 36, 126, 92, 191, 156]}
+    src_dec = ptr_table([addr(s, j) for s in range(B) for j in range(1, k + 1)])
+    dst_dec = ptr_table([addr(s, 0) for s in range(B)])
+    src_cp = ptr_table([addr(s, i) for s in range(B) for i in range(7)])
+    dst_cp = ptr_table([addr(s, 7 + i) for s in range(B) for i in range(7)])
+    stream = torch.cuda.current_stream().cuda_stream
+
+    variants = []
+    for vec in (1, 2, 4):
+        variants.append((f"copy vec{vec}", 1, 1, 1, vec, 0, None, None, src_cp, dst_cp, 7 * B, 0, 0, 2 * S * 7 * B))
+    for vec in (1, 2, 4):
+        for mode, mname in ((0, "table"), (1, "mask"), (2, "allperm"), (3, "xoronly")):
+            variants.append((f"enc perm vec{vec} {mname}", 0, 10, 4, vec, mode, q_enc, n_enc, src_enc, dst_enc, B,
+                             u_enc, z_enc, (k + m) * S * B))
+    variants.append(("enc lds", 2, 10, 4, 1, 0, q_enc, n_enc, src_enc, dst_enc, B, u_enc, z_enc, (k + m) * S * B))
+    for name, row in dec_rows.items():
+        qd, nd = tables(row)
+        ud, zd = masks(row)
+        for vec in (1, 2, 4):
+            variants.append((f"dec1 {name} vec{vec} mask", 0, 10, 1, vec, 1, qd, nd, src_dec, dst_dec, B, ud, zd,
+                             (k + 1) * S * B))
+        variants.append((f"dec1 {name} lds", 2, 10, 1, 1, 0, qd, nd, src_dec, dst_dec, B, ud, zd, (k + 1) * S * B))
+
+    times = {v[0]: [] for v in variants}
+    for nt in (1,):
+        for rnd in range(args.rounds + 2):
+            for v in variants:
+                name, var, K, R, vec, mode, qt, nb, st, dt, stripes, um, zm, nbytes = v
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                rc = L.ecgpu_diag_launch(var, K, R, vec, mode, qt.data_ptr() if qt is not None else None,
+                                         nb.data_ptr() if nb is not None else None, st.data_ptr(), dt.data_ptr(),
+                                         stripes, S, um, zm, nt, stream)
+                e1.record()
+                assert rc == 0, (name, rc)
+                torch.cuda.synchronize()
+                if rnd >= 2:
+                    times[name].append(e0.elapsed_time(e1))
+    for v in variants:
+        t = times[v[0]]
+        med = statistics.median(t)
+        print(json.dumps({"variant": v[0], "median_ms": round(med, 4), "min_ms": round(min(t), 4),
+                          "GBps_median": round(v[-1] / med / 1e6, 1), "GBps_best": round(v[-1] / min(t) / 1e6, 1)}))
+
+
+if __name__ == "__main__":
+    main()

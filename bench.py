@@ -137,12 +137,11 @@ def main():
     k, m, S, B = K_DATA, M_PARITY, SHARD, args.stripes
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
 
-    # [B][k+m][S] in one HBM slab; random data (LDS/perm paths are data-independent,
-    # but zeros would under-state DVFS and HBM behaviour).
-    slab = torch.empty((B, k + m, S), dtype=torch.uint8, device=dev)
+    # B stripes x (k+m) shards in one HBM slab at the library's recommended
+    # shard stride (S + 4 KiB skew); random data (zeros would flatter DVFS).
+    slab, shards = E.alloc_stripes(B, k, m, S, dev)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    slab[:, :k].random_(0, 256, generator=g)
-    shards = [[slab[s, i] for i in range(k + m)] for s in range(B)]
+    slab.random_(0, 256, generator=g)
 
     kind = N.KERNEL_LDS if args.kernel == "lds" else N.KERNEL_PERM
     enc = E.encode_plan(k, m, M, local).bind([st[:k] for st in shards], [st[k:] for st in shards], S)
@@ -187,10 +186,10 @@ def main():
     # every step from the survivors; compare with an independent encode check)
     ok = True
     if rank == 0:
-        chk = torch.empty_like(slab[0, k:])
+        chk = torch.empty((m, S), dtype=torch.uint8, device=dev)
         E.encode_plan(k, m, M, local).bind([shards[0][:k]], [[chk[i] for i in range(m)]], S).launch(stream.cuda_stream)
         torch.cuda.synchronize(dev)
-        ok = bool(torch.equal(chk, slab[0, k:]))
+        ok = all(bool(torch.equal(chk[i], shards[0][k + i])) for i in range(m))
 
     workload = f"RS(10,4) encode + decode{{0}}, 4 MiB shards, {B} stripes/GPU"
     if rank == 0:
@@ -213,6 +212,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic (uniform random bytes, device-generated)",
             "config": {"workload": workload, "k": k, "m": m, "shard_bytes": S, "stripes_per_gpu": B,
+                       "shard_stride_bytes": int(slab.stride(1)),
                        "erasures": [0], "kernel": args.kernel, "nontemporal": bool(args.nt),
                        "parallelism": f"stripes sharded over {world} GPU(s), no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -15,6 +15,11 @@ extern "C" {
 ECGPU_API const char* ecgpu_version(void) { return "ecgpu 0.1 (gfx950)"; }
 ECGPU_API void ecgpu_free(void* p) { std::free(p); }
 
+ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size) {
+  if (size < 0) size = 0;
+  return ((size + 255) & ~int64_t(255)) + 4096;
+}
+
 ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w) { return single_multiply(a, b, w); }
 ECGPU_API int ecgpu_galois_single_divide(int a, int b, int w) { return single_divide(a, b, w); }
 ECGPU_API int ecgpu_galois_inverse(int a, int w) { return inverse(a, w); }

@@ -42,6 +42,20 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
     if (K == 10 && R == 1) fn = pick_vec<10, 1>(vec, mode);
   } else if (variant == 1) {
     fn = vec == 1 ? &ecgpu::dev::diag_copy<1> : vec == 2 ? &ecgpu::dev::diag_copy<2> : &ecgpu::dev::diag_copy<4>;
+  } else if (variant == 3) {
+    // persistent streaming form; `vec` = blocks per stripe
+    if (K == 10 && R == 4) fn = mode == 3 ? &ecgpu::dev::gf_apply_perm_stream<10, 4, 3>
+                                          : &ecgpu::dev::gf_apply_perm_stream<10, 4, 2>;
+    if (K == 10 && R == 1) fn = mode == 3 ? &ecgpu::dev::gf_apply_perm_stream<10, 1, 3>
+                                          : &ecgpu::dev::gf_apply_perm_stream<10, 1, 2>;
+  } else if (variant == 4) {
+    // production gf_apply; `mode` = UnitMask
+    vec = 1;
+    if (K == 10 && R == 4)
+      fn = mode == 0 ? &ecgpu::dev::gf_apply<10, 4, 0> : mode == 1 ? &ecgpu::dev::gf_apply<10, 4, 1>
+                                                        : &ecgpu::dev::gf_apply<10, 4, 3>;
+    if (K == 10 && R == 1)
+      fn = mode == 4 ? &ecgpu::dev::gf_apply<10, 1, 4> : &ecgpu::dev::gf_apply<10, 1, 0>;
   } else if (variant == 2) {
     vec = 1;
     if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_lds<10, 4>;
@@ -66,6 +80,7 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
   a.nt = nt;
   const long long per_block = 256LL * vec;
   dim3 grid(unsigned((a.nvec + per_block - 1) / per_block), unsigned(stripes));
+  if (variant == 3) grid = dim3(unsigned(vec), unsigned(stripes));
   void* args[] = {&a};
   return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(256), args, 0,
                          static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -3;

@@ -59,31 +59,55 @@ int env_int(const char* name, int dflt) {
 // ------------------------------------------------------- kernel tables ----
 using KernelFn = void (*)(ApplyArgs);
 
-// Production kernel shape (chosen by A/B on MI355X):
-// one 16-B column per lane, 0/1 coefficients classified by kernarg masks.
-constexpr int kProdVec = 1;
-constexpr int kProdMode = dev::kClassFromMask;
-
-template <int K, int R>
-constexpr KernelFn perm_fn() { return &dev::gf_apply_perm<K, R, kProdVec, kProdMode>; }
+// Production kernel (A/B-chosen on MI355X): one 16-B column
+// per lane, v_perm multiply, XOR3 via v_bitop3, unit-coefficient structure
+// specialised at compile time (gf_kernels.hpp, UnitMask).
+template <int K, int R, int U>
+constexpr KernelFn apply_fn() { return &dev::gf_apply<K, R, U>; }
 template <int K, int R>
 constexpr KernelFn lds_fn() { return &dev::gf_apply_lds<K, R>; }
 
+constexpr int kUnitVariants[5] = {dev::kUnitNone, dev::kUnitCol0, dev::kUnitRow0, dev::kUnitCol0 | dev::kUnitRow0,
+                                  dev::kUnitAll};
+
+template <int K, int R>
+struct Cell {
+  static constexpr KernelFn apply[5] = {apply_fn<K, R, kUnitVariants[0]>(), apply_fn<K, R, kUnitVariants[1]>(),
+                                        apply_fn<K, R, kUnitVariants[2]>(), apply_fn<K, R, kUnitVariants[3]>(),
+                                        apply_fn<K, R, kUnitVariants[4]>()};
+};
+
 template <int K>
 struct Row {
-  static constexpr KernelFn perm[4] = {perm_fn<K, 1>(), perm_fn<K, 2>(), perm_fn<K, 3>(), perm_fn<K, 4>()};
+  static constexpr const KernelFn* apply[4] = {Cell<K, 1>::apply, Cell<K, 2>::apply, Cell<K, 3>::apply,
+                                               Cell<K, 4>::apply};
   static constexpr KernelFn lds[4] = {lds_fn<K, 1>(), lds_fn<K, 2>(), lds_fn<K, 3>(), lds_fn<K, 4>()};
 };
 
 template <int... Ks>
 struct Table {
-  static KernelFn get(bool lds, int K, int R) {
+  // unit_variant indexes kUnitVariants
+  static KernelFn get(bool lds, int K, int R, int unit_variant) {
     KernelFn out = nullptr;
-    ((K == Ks ? (out = lds ? Row<Ks>::lds[R - 1] : Row<Ks>::perm[R - 1], 0) : 0), ...);
+    ((K == Ks ? (out = lds ? Row<Ks>::lds[R - 1] : Row<Ks>::apply[R - 1][unit_variant], 0) : 0), ...);
     return out;
   }
 };
 using SpecTable = Table<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
+
+// Which compile-time unit structure holds exactly for rows [r0, r0+R).
+int unit_variant(const std::vector<uint8_t>& coef, int K, int r0, int R) {
+  bool all = true, col0 = true, row0 = true;
+  for (int r = 0; r < R; ++r)
+    for (int j = 0; j < K; ++j) {
+      const bool one = coef[size_t(r0 + r) * K + j] == 1;
+      all &= one;
+      if (j == 0) col0 &= one;
+      if (r == 0) row0 &= one;
+    }
+  if (all) return 4;
+  return (col0 ? 1 : 0) | (row0 ? 2 : 0);
+}
 
 KernelFn generic_fn(int R) {
   switch (R) {
@@ -220,8 +244,9 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
   for (int r0 = 0; r0 < p->rows; r0 += dev::kMaxRows) {
     const int R = std::min(dev::kMaxRows, p->rows - r0);
     const bool spec = K <= dev::kMaxSpecK;
-    KernelFn vec_fn = spec ? SpecTable::get(p->kind == ECGPU_KERNEL_LDS, K, R) : generic_fn(R);
-    const int vec = (spec && p->kind != ECGPU_KERNEL_LDS) ? kProdVec : 1;
+    KernelFn vec_fn = spec ? SpecTable::get(p->kind == ECGPU_KERNEL_LDS, K, R, unit_variant(p->coef, K, r0, R))
+                           : generic_fn(R);
+    const int vec = 1;
     uint64_t unit = 0, zero = 0;
     if (spec)
       for (int r = 0; r < R; ++r)

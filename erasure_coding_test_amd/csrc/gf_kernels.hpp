@@ -69,13 +69,17 @@ __device__ __forceinline__ uint32_t gf_mul_perm(const u32x4& q, uint32_t s0, uin
   return perm_lookup(q.x, s0) ^ perm_lookup(q.y, s1) ^ perm_lookup(q.z, s2) ^ perm_lookup(q.w, s3);
 }
 
+// Shards live in global memory: address space 1 makes these global_load /
+// global_store (not flat_*, which also arbitrates the LDS aperture).
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+
 __device__ __forceinline__ u32x4 load16(const uint8_t* p, int64_t col, int nt) {
-  const u32x4* a = reinterpret_cast<const u32x4*>(p) + col;
+  const gu32x4* a = (const gu32x4*)p + col;  // C cast: generic -> global address space
   return nt ? __builtin_nontemporal_load(a) : *a;
 }
 
 __device__ __forceinline__ void store16(uint8_t* p, int64_t col, const u32x4& v, int nt) {
-  u32x4* a = reinterpret_cast<u32x4*>(p) + col;
+  gu32x4* a = (gu32x4*)p + col;
   if (nt)
     __builtin_nontemporal_store(v, a);
   else
@@ -83,8 +87,10 @@ __device__ __forceinline__ void store16(uint8_t* p, int64_t col, const u32x4& v,
 }
 
 // acc ^= c * v for one 16-byte column; sel = the four 2-bit selector words.
-template <int MODE>
-__device__ __forceinline__ void mac16(const ApplyArgs& a, int idx, const u32x4& v, const u32x4 (&sel)[4], u32x4& acc) {
+// Tables come from `qt` (global qtab, or the block's LDS copy).
+template <int MODE, typename QPtr>
+__device__ __forceinline__ void mac16(const ApplyArgs& a, QPtr qt, int idx, const u32x4& v, const u32x4 (&sel)[4],
+                                      u32x4& acc) {
   if (MODE == kXorOnly) {
     acc ^= v;
     return;
@@ -96,7 +102,7 @@ __device__ __forceinline__ void mac16(const ApplyArgs& a, int idx, const u32x4& 
       return;
     }
   }
-  const u32x4 q = a.qtab[idx];
+  const u32x4 q = qt[idx];
   if (MODE == kClassFromTable) {
     if (q.x == 0u) return;      // coefficient 0
     if (q.x == kQ0Unit) {       // coefficient 1
@@ -109,6 +115,8 @@ __device__ __forceinline__ void mac16(const ApplyArgs& a, int idx, const u32x4& 
   acc.z ^= gf_mul_perm(q, sel[0].z, sel[1].z, sel[2].z, sel[3].z);
   acc.w ^= gf_mul_perm(q, sel[0].w, sel[1].w, sel[2].w, sel[3].w);
 }
+
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
 
 // ---------------------------------------------------------------- PERM ----
 // Lane l of block b handles 16-byte columns b*VEC*256 + v*256 + l (v < VEC)
@@ -158,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm(ApplyArgs a) {
         sel[3] = (xv >> 6) & kLo2;
       }
 #pragma unroll
-      for (int r = 0; r < R; ++r) mac16<MODE>(a, r * K + j, xv, sel, acc[v][r]);
+      for (int r = 0; r < R; ++r) mac16<MODE>(a, a.qtab, r * K + j, xv, sel, acc[v][r]);
     }
   }
 
@@ -174,6 +182,145 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm(ApplyArgs a) {
       if (live[v])
 #pragma unroll
         for (int r = 0; r < R; ++r) store16(dp[r], col0 + v * kBlock, acc[v][r], 0);
+  }
+}
+
+// ------------------------------------------------- PERM, production ----
+// Unit-coefficient structure known at compile time (host checks it exactly):
+//   kUnitCol0 -- coefficient (r, 0) == 1 for every row of the launch
+//   kUnitRow0 -- coefficient (0, j) == 1 for every source (launch row 0)
+//   kUnitAll  -- every coefficient == 1 (pure XOR, e.g. decode of one data
+//                shard with the all-ones parity row)
+// reed_sol_vandermonde_coding_matrix always has row 0 and column 0 all ones
+// (reed_sol.cpp:324-349), so RS encode launches take kUnitCol0|kUnitRow0.
+// A unit term costs one XOR and no selectors; every other term is 4 v_perm
+// + 2 v_bitop3 (XOR3) per dword.
+enum UnitMask : int { kUnitNone = 0, kUnitCol0 = 1, kUnitRow0 = 2, kUnitAll = 4 };
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+template <int UNITS>
+__device__ __forceinline__ constexpr bool is_unit(int r, int j) {
+  return (UNITS & kUnitAll) || ((UNITS & kUnitCol0) && j == 0) || ((UNITS & kUnitRow0) && r == 0);
+}
+
+__device__ __forceinline__ uint32_t mac_word(uint32_t acc, const u32x4& q, uint32_t x) {
+  const uint32_t s0 = x & kLo2, s1 = (x >> 2) & kLo2, s2 = (x >> 4) & kLo2, s3 = (x >> 6) & kLo2;
+  return xor3(acc, xor3(perm_lookup(q.x, s0), perm_lookup(q.y, s1), perm_lookup(q.z, s2)), perm_lookup(q.w, s3));
+}
+
+template <int K, int R, int UNITS>
+__global__ __launch_bounds__(kBlock) void gf_apply(ApplyArgs a) {
+  const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+
+  u32x4 x[K];
+  if (a.nt) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, 1);
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, 0);
+  }
+
+  u32x4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (is_unit<UNITS>(r, j)) {
+        acc[r] ^= x[j];
+      } else {
+        const u32x4 q = a.qtab[r * K + j];
+        acc[r].x = mac_word(acc[r].x, q, x[j].x);
+        acc[r].y = mac_word(acc[r].y, q, x[j].y);
+        acc[r].z = mac_word(acc[r].z, q, x[j].z);
+        acc[r].w = mac_word(acc[r].w, q, x[j].w);
+      }
+    }
+  }
+
+  if (a.nt) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], 1);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], 0);
+  }
+}
+
+// ------------------------------------------------------ PERM, streaming ----
+// Persistent-per-stripe form: gridDim.x blocks share one stripe, block b
+// walks a CONTIGUOUS run of columns [b*chunk, (b+1)*chunk) 256 columns at a
+// time, and the K loads of step i+1 are issued before step i is computed and
+// stored (register double buffer), so every wave keeps K*16 B per lane in
+// flight while it computes.  Each shard is then read as gridDim.x long
+// sequential streams instead of interleaved 4 KiB pieces.
+template <int K, int R, int MODE>
+__global__ __launch_bounds__(kBlock) void gf_apply_perm_stream(ApplyArgs a) {
+  __shared__ u32x4 lq[R * K];
+  for (int i = threadIdx.x; i < R * K; i += kBlock) lq[i] = a.qtab[i];
+  __syncthreads();
+  const int s = blockIdx.y;
+  const int64_t steps_total = (a.nvec + kBlock - 1) / kBlock;
+  const int64_t steps_per_block = (steps_total + gridDim.x - 1) / gridDim.x;
+  const int64_t step0 = int64_t(blockIdx.x) * steps_per_block;
+  const int64_t step_end = step0 + steps_per_block < steps_total ? step0 + steps_per_block : steps_total;
+  if (step0 >= step_end) return;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+  const uint8_t* src[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) src[j] = sp[j];
+
+  u32x4 cur[K], nxt[K];
+  int64_t col = step0 * kBlock + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < K; ++j) cur[j] = col < a.nvec ? load16(src[j], col, a.nt) : u32x4{0u, 0u, 0u, 0u};
+  for (int64_t step = step0; step < step_end; ++step) {
+    const int64_t ncol = col + kBlock;
+    const bool more = step + 1 < step_end;
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) nxt[j] = ncol < a.nvec ? load16(src[j], ncol, a.nt) : u32x4{0u, 0u, 0u, 0u};
+    }
+    u32x4 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+    // Re-read the tables from LDS every step (uniform address: broadcast
+    // ds_read_b128).  Hoisted out of the loop they would be parked in
+    // R*K*4 VGPRs and cut occupancy to 2 waves/SIMD.
+    lds_u32x4* qt = (lds_u32x4*)lq;
+    asm volatile("" : "+v"(qt));
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const u32x4 xv = cur[j];
+      u32x4 sel[4];
+      if (MODE != kXorOnly) {
+        sel[0] = xv & kLo2;
+        sel[1] = (xv >> 2) & kLo2;
+        sel[2] = (xv >> 4) & kLo2;
+        sel[3] = (xv >> 6) & kLo2;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) mac16<MODE>(a, qt, r * K + j, xv, sel, acc[r]);
+    }
+    if (col < a.nvec) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], a.nt);
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) cur[j] = nxt[j];
+    }
+    col = ncol;
   }
 }
 

@@ -64,6 +64,18 @@ class StripePlan:
             pass
 
 
+def alloc_stripes(stripes: int, k: int, m: int, size: int, device=None):
+    """One HBM slab for `stripes` stripes of k+m shards, laid out with the
+    library's recommended shard stride (ecgpu_recommended_shard_stride: a
+    4 KiB skew so a column's k+m accesses do not share an HBM bank).
+    Returns (slab, shards) with shards[s][i] a `size`-byte uint8 view."""
+    stride = int(N.lib.ecgpu_recommended_shard_stride(size))
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    slab = torch.empty((stripes, k + m, stride), dtype=torch.uint8, device=dev)
+    shards = [[slab[s, i, :size] for i in range(k + m)] for s in range(stripes)]
+    return slab, shards
+
+
 def encode_plan(k: int, m: int, matrix: Sequence[int], device: int = -1) -> StripePlan:
     """Plan computing the m coding shards from the k data shards of each stripe."""
     return StripePlan(m, k, matrix, device)

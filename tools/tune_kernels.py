@@ -54,9 +54,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--stripes", type=int, default=24)
+    ap.add_argument("--pads", default="0", help="comma list of per-shard padding bytes (shard stride = S + pad)")
+    ap.add_argument("--only", default="", help="substring filter on variant names")
     args = ap.parse_args()
     k, m, S, B = 10, 4, 4 << 20, args.stripes
-    slab = torch.empty((B, k + m, S), dtype=torch.uint8, device="cuda")
+    results = []
+    for pad in [int(p) for p in args.pads.split(",")]:
+        results += run_layout(args, k, m, S, B, pad)
+    for r in results:
+        print(json.dumps(r))
+
+
+def run_layout(args, k, m, S, B, pad):
+    slab = torch.empty((B, k + m, S + pad), dtype=torch.uint8, device="cuda")
     slab.random_(0, 256, generator=torch.Generator(device="cuda").manual_seed(5))
     addr = lambda s, i: slab[s, i].data_ptr()
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
@@ -72,26 +82,40 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     variants = []
-    for vec in (1, 2, 4):
-        variants.append((f"copy vec{vec}", 1, 1, 1, vec, 0, None, None, src_cp, dst_cp, 7 * B, 0, 0, 2 * S * 7 * B))
-    for vec in (1, 2, 4):
-        for mode, mname in ((0, "table"), (1, "mask"), (2, "allperm"), (3, "xoronly")):
-            variants.append((f"enc perm vec{vec} {mname}", 0, 10, 4, vec, mode, q_enc, n_enc, src_enc, dst_enc, B,
-                             u_enc, z_enc, (k + m) * S * B))
-    variants.append(("enc lds", 2, 10, 4, 1, 0, q_enc, n_enc, src_enc, dst_enc, B, u_enc, z_enc, (k + m) * S * B))
+    for nt in (1, 0):
+        variants.append((f"copy vec1 nt{nt}", 1, 1, 1, 1, 0, None, None, src_cp, dst_cp, 7 * B, 0, 0,
+                         2 * S * 7 * B, nt))
+        for vec in (1, 2):
+            for mode, mname in ((2, "allperm"), (3, "xoronly")):
+                variants.append((f"enc perm vec{vec} {mname} nt{nt}", 0, 10, 4, vec, mode, q_enc, n_enc, src_enc,
+                                 dst_enc, B, u_enc, z_enc, (k + m) * S * B, nt))
+        for bps in (16, 32, 64, 128):
+            for mode, mname in ((2, "allperm"), (3, "xoronly")):
+                variants.append((f"enc stream bps{bps} {mname} nt{nt}", 3, 10, 4, bps, mode, q_enc, n_enc, src_enc,
+                                 dst_enc, B, u_enc, z_enc, (k + m) * S * B, nt))
+    for nt in (1, 0):
+        for um, uname in ((0, "none"), (1, "col0"), (3, "rs")):
+            variants.append((f"enc apply {uname} nt{nt}", 4, 10, 4, 1, um, q_enc, n_enc, src_enc, dst_enc, B, u_enc,
+                             z_enc, (k + m) * S * B, nt))
+    variants.append(("enc lds nt1", 2, 10, 4, 1, 0, q_enc, n_enc, src_enc, dst_enc, B, u_enc, z_enc,
+                     (k + m) * S * B, 1))
     for name, row in dec_rows.items():
         qd, nd = tables(row)
         ud, zd = masks(row)
-        for vec in (1, 2, 4):
-            variants.append((f"dec1 {name} vec{vec} mask", 0, 10, 1, vec, 1, qd, nd, src_dec, dst_dec, B, ud, zd,
-                             (k + 1) * S * B))
-        variants.append((f"dec1 {name} lds", 2, 10, 1, 1, 0, qd, nd, src_dec, dst_dec, B, ud, zd, (k + 1) * S * B))
+        variants.append((f"dec1 {name} vec1 allperm nt1", 0, 10, 1, 1, 2, qd, nd, src_dec, dst_dec, B, ud, zd,
+                         (k + 1) * S * B, 1))
+        variants.append((f"dec1 {name} apply {'all' if name == 'ones' else 'none'} nt1", 4, 10, 1, 1,
+                         4 if name == "ones" else 0, qd, nd, src_dec, dst_dec, B, ud, zd, (k + 1) * S * B, 1))
+        for bps in (32, 64):
+            variants.append((f"dec1 {name} stream bps{bps} nt1", 3, 10, 1, bps, 2, qd, nd, src_dec, dst_dec, B, ud,
+                             zd, (k + 1) * S * B, 1))
 
+    variants = [v for v in variants if args.only in v[0]]
     times = {v[0]: [] for v in variants}
-    for nt in (1,):
+    if True:
         for rnd in range(args.rounds + 2):
             for v in variants:
-                name, var, K, R, vec, mode, qt, nb, st, dt, stripes, um, zm, nbytes = v
+                name, var, K, R, vec, mode, qt, nb, st, dt, stripes, um, zm, nbytes, nt = v
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 rc = L.ecgpu_diag_launch(var, K, R, vec, mode, qt.data_ptr() if qt is not None else None,
@@ -102,11 +126,15 @@ def main():
                 torch.cuda.synchronize()
                 if rnd >= 2:
                     times[name].append(e0.elapsed_time(e1))
+    out = []
     for v in variants:
         t = times[v[0]]
         med = statistics.median(t)
-        print(json.dumps({"variant": v[0], "median_ms": round(med, 4), "min_ms": round(min(t), 4),
-                          "GBps_median": round(v[-1] / med / 1e6, 1), "GBps_best": round(v[-1] / min(t) / 1e6, 1)}))
+        out.append({"variant": v[0], "pad": pad, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
+                    "GBps_median": round(v[-2] / med / 1e6, 1), "GBps_best": round(v[-2] / min(t) / 1e6, 1)})
+    del slab
+    torch.cuda.empty_cache()
+    return out
 
 
 if __name__ == "__main__":

@@ -1,0 +1,173 @@
+"""Host-memory (PCIe-inclusive) and per-config measurements for DESIGN.md.
+
+Not the headline (bench.py is); these are the rates a caller whose shards
+originate and terminate in host memory sees, and the other BASELINE configs.
+
+  e2e_pinned   RS(10,4) 4 MiB stripes in pinned host memory: H2D of the 10
+               data shards on a copy stream, encode on the compute stream,
+               D2H of the 4 parity shards on a second copy stream; 3-deep
+               ring of device stripe buffers so copies overlap compute.
+  dropin_pageable  jerasure_matrix_encode / _decode straight on malloc'd
+               (pageable) numpy buffers through the C ABI -- the reference
+               client's call shape (client_main.cpp:1060, :2118).
+  configs      device-resident C2 RS(6,3) 1 MiB, C3 decode{0}, C4 decode
+               {0,1,2,3}, C5 RS(12,4) 16 MiB encode (kernel time, HBM GB/s).
+  pcie         raw pinned H2D / D2H copy rates (the ceiling for e2e).
+
+    python tools/bench_e2e.py [--stripes 48]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import erasure_coding_test_amd as E  # noqa: E402
+
+GiB = 2**30
+
+
+def timed_events(fn, reps=10, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / 1e3)
+    return statistics.median(ts)
+
+
+def pcie_rates(nbytes=1 << 30):
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    h2d = timed_events(lambda: d.copy_(h, non_blocking=True), reps=5)
+    d2h = timed_events(lambda: h.copy_(d, non_blocking=True), reps=5)
+    return {"h2d_GBps": round(nbytes / h2d / 1e9, 1), "d2h_GBps": round(nbytes / d2h / 1e9, 1)}
+
+
+def e2e_pinned(stripes=48, k=10, m=4, S=4 << 20, ring=3):
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    host = torch.empty((stripes, k + m, S), dtype=torch.uint8).pin_memory()
+    host[:, :k].random_(0, 256)
+    slabs = []
+    for _ in range(ring):
+        slab, shards = E.alloc_stripes(1, k, m, S)
+        plan = E.encode_plan(k, m, M).bind([shards[0][:k]], [shards[0][k:]], S)
+        slabs.append((slab, shards[0], plan))
+    comp = torch.cuda.current_stream()
+    h2d, d2h = torch.cuda.Stream(), torch.cuda.Stream()
+    loaded = [torch.cuda.Event() for _ in range(ring)]
+    computed = [torch.cuda.Event() for _ in range(ring)]
+    drained = [torch.cuda.Event() for _ in range(ring)]
+
+    def run():
+        for s in range(stripes):
+            r = s % ring
+            _, sh, plan = slabs[r]
+            with torch.cuda.stream(h2d):
+                h2d.wait_event(drained[r])
+                for j in range(k):
+                    sh[j].copy_(host[s, j], non_blocking=True)
+                loaded[r].record(h2d)
+            comp.wait_event(loaded[r])
+            plan.launch(comp.cuda_stream)
+            computed[r].record(comp)
+            with torch.cuda.stream(d2h):
+                d2h.wait_event(computed[r])
+                for i in range(m):
+                    host[s, k + i].copy_(sh[k + i], non_blocking=True)
+                drained[r].record(d2h)
+        torch.cuda.synchronize()
+
+    run()
+    t0 = time.perf_counter()
+    run()
+    t = time.perf_counter() - t0
+    # correctness of the streamed parity for one stripe
+    ref = torch.empty((m, S), dtype=torch.uint8, device="cuda")
+    d = host[stripes - 1, :k].cuda()
+    E.encode_plan(k, m, M).bind([[d[j] for j in range(k)]], [[ref[i] for i in range(m)]], S).launch()
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(ref.cpu(), host[stripes - 1, k:]))
+    return {"workload": f"RS(10,4) 4 MiB encode, {stripes} stripes pinned host -> HBM -> pinned host",
+            "data_GiBps": round(stripes * k * S / t / GiB, 2),
+            "pcie_bytes_GBps": round(stripes * (k + m) * S / t / 1e9, 1), "parity_ok": ok}
+
+
+def dropin_pageable(k=10, m=4, S=4 << 20, reps=5):
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    rng = np.random.default_rng(0)
+    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+    coding = [np.zeros(S, np.uint8) for _ in range(m)]
+    E.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, S)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        E.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, S)
+    te = (time.perf_counter() - t0) / reps
+    bufs = data + coding
+    saved = bufs[0].copy()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        bufs[0][:] = 0
+        E.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, [0], bufs[:k], bufs[k:], S)
+    td = (time.perf_counter() - t0) / reps
+    return {"workload": "jerasure_matrix_encode/decode{0} on pageable malloc buffers, RS(10,4) 4 MiB, synchronous",
+            "encode_ms": round(te * 1e3, 2), "encode_data_GiBps": round(k * S / te / GiB, 2),
+            "decode_ms": round(td * 1e3, 2), "decode_ok": bool(np.array_equal(bufs[0], saved))}
+
+
+def device_configs():
+    out = []
+    cases = [("C2 RS(6,3) 1 MiB encode", 6, 3, 1 << 20, 96, None),
+             ("C3 RS(10,4) 4 MiB decode{0}", 10, 4, 4 << 20, 24, [0]),
+             ("C4 RS(10,4) 4 MiB decode{0,1,2,3}", 10, 4, 4 << 20, 24, [0, 1, 2, 3]),
+             ("C5 RS(12,4) 16 MiB encode", 12, 4, 16 << 20, 8, None)]
+    for name, k, m, S, B, er in cases:
+        M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+        slab, shards = E.alloc_stripes(B, k, m, S)
+        slab.random_(0, 256)
+        E.encode_plan(k, m, M).bind([st[:k] for st in shards], [st[k:] for st in shards], S).launch()
+        if er is None:
+            p = E.encode_plan(k, m, M).bind([st[:k] for st in shards], [st[k:] for st in shards], S)
+            nbytes, data = (k + m) * S * B, k * S * B
+        else:
+            t0 = time.perf_counter()
+            p = E.DecodePlan(k, m, M, er)
+            plan_us = (time.perf_counter() - t0) * 1e6
+            p.bind_stripes(shards, S)
+            nbytes, data = (len(p.src_ids) + len(p.out_ids)) * S * B, k * S * B
+        t = timed_events(p.launch)
+        rec = {"config": name, "stripes": B, "launch_ms": round(t * 1e3, 4), "hbm_GBps": round(nbytes / t / 1e9, 1),
+               "frac_of_8TBps": round(nbytes / t / 8e12, 4), "data_GiBps": round(data / t / GiB, 1)}
+        if er is not None:
+            rec["host_plan_us"] = round(plan_us, 1)
+        out.append(rec)
+        del slab, shards, p
+        torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stripes", type=int, default=48)
+    a = ap.parse_args()
+    res = {"pcie": pcie_rates(), "e2e_pinned": e2e_pinned(a.stripes), "dropin_pageable": dropin_pageable(),
+           "device_configs": device_configs()}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -48,7 +48,7 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
                                           : &ecgpu::dev::gf_apply_perm_stream<10, 4, 2>;
     if (K == 10 && R == 1) fn = mode == 3 ? &ecgpu::dev::gf_apply_perm_stream<10, 1, 3>
                                           : &ecgpu::dev::gf_apply_perm_stream<10, 1, 2>;
-  } else if (variant == 4) {
+  } else if (variant == 4 || variant == 5) {
     // production gf_apply; `mode` = UnitMask
     vec = 1;
     if (K == 10 && R == 4)
@@ -56,6 +56,18 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
                                                         : &ecgpu::dev::gf_apply<10, 4, 3>;
     if (K == 10 && R == 1)
       fn = mode == 4 ? &ecgpu::dev::gf_apply<10, 1, 4> : &ecgpu::dev::gf_apply<10, 1, 0>;
+  } else if (variant == 6) {
+    vec = 1;
+    if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_occ8<10, 4, 3>;
+    if (K == 10 && R == 1) fn = mode == 4 ? &ecgpu::dev::gf_apply_occ8<10, 1, 4> : &ecgpu::dev::gf_apply_occ8<10, 1, 0>;
+  } else if (variant == 7) {
+    // production body; vec bit0 = stripe-fastest order, bit1 = 8-wave register cap; mode = UnitMask
+    const bool occ8 = (vec & 2) != 0;
+    if (K == 10 && R == 4)
+      fn = occ8 ? &ecgpu::dev::gf_apply_occ8<10, 4, 3> : &ecgpu::dev::gf_apply<10, 4, 3>;
+    if (K == 10 && R == 1)
+      fn = mode == 4 ? (occ8 ? &ecgpu::dev::gf_apply_occ8<10, 1, 4> : &ecgpu::dev::gf_apply<10, 1, 4>)
+                     : (occ8 ? &ecgpu::dev::gf_apply_occ8<10, 1, 0> : &ecgpu::dev::gf_apply<10, 1, 0>);
   } else if (variant == 2) {
     vec = 1;
     if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_lds<10, 4>;
@@ -78,9 +90,18 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
   a.K = K;
   a.R = R;
   a.nt = nt;
-  const long long per_block = 256LL * vec;
+  const long long per_block = 256LL * (variant == 0 || variant == 1 ? vec : 1);
   dim3 grid(unsigned((a.nvec + per_block - 1) / per_block), unsigned(stripes));
   if (variant == 3) grid = dim3(unsigned(vec), unsigned(stripes));
+  if (variant == 7) {
+    a.stripe_fast = vec & 1;
+    grid = a.stripe_fast ? dim3(unsigned(stripes), unsigned((a.nvec + 255) / 256))
+                         : dim3(unsigned((a.nvec + 255) / 256), unsigned(stripes));
+  }
+  if (variant == 5) {  // stripe-fastest block order
+    a.stripe_fast = 1;
+    grid = dim3(unsigned(stripes), unsigned((a.nvec + 255) / 256));
+  }
   void* args[] = {&a};
   return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(256), args, 0,
                          static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -3;

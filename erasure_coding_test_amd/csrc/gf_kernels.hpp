@@ -50,6 +50,7 @@ struct ApplyArgs {
   int src_stride, dst_stride, row0;  // row0 = first dst column of this launch
   int K, R;                       // runtime copies (generic / byte kernels)
   int nt;                         // 1: non-temporal loads/stores
+  int stripe_fast;                // 1: blockIdx.x = stripe, blockIdx.y = column block
 };
 
 // How a launch treats coefficients 0 and 1.
@@ -128,7 +129,9 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm(ApplyArgs a) {
   if (col0 >= a.nvec) return;
   const int s = blockIdx.y;
   const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
-  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+  uint8_t* dp[R];  // all pointers before the first store (see gf_apply_body)
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
 
   bool live[VEC];
 #pragma unroll
@@ -212,12 +215,18 @@ __device__ __forceinline__ uint32_t mac_word(uint32_t acc, const u32x4& q, uint3
 }
 
 template <int K, int R, int UNITS>
-__global__ __launch_bounds__(kBlock) void gf_apply(ApplyArgs a) {
-  const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+__device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
+  const unsigned cblk = a.stripe_fast ? blockIdx.y : blockIdx.x;
+  const int s = a.stripe_fast ? blockIdx.x : blockIdx.y;
+  const int64_t col = int64_t(cblk) * kBlock + threadIdx.x;
   if (col >= a.nvec) return;
-  const int s = blockIdx.y;
   const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
-  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+  // Fetch ALL pointers before the first store: a pointer read after a store
+  // cannot use the scalar cache (not coherent with vector stores), and the
+  // compiler then chains one dependent global load per output row.
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
 
   u32x4 x[K];
   if (a.nt) {
@@ -256,6 +265,17 @@ __global__ __launch_bounds__(kBlock) void gf_apply(ApplyArgs a) {
   }
 }
 
+template <int K, int R, int UNITS>
+__global__ __launch_bounds__(kBlock) void gf_apply(ApplyArgs a) {
+  gf_apply_body<K, R, UNITS>(a);
+}
+
+// Same body, register budget capped for 8 waves/SIMD (<= 64 VGPRs).
+template <int K, int R, int UNITS>
+__global__ __launch_bounds__(kBlock, 8) void gf_apply_occ8(ApplyArgs a) {
+  gf_apply_body<K, R, UNITS>(a);
+}
+
 // ------------------------------------------------------ PERM, streaming ----
 // Persistent-per-stripe form: gridDim.x blocks share one stripe, block b
 // walks a CONTIGUOUS run of columns [b*chunk, (b+1)*chunk) 256 columns at a
@@ -275,7 +295,9 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm_stream(ApplyArgs a) {
   const int64_t step_end = step0 + steps_per_block < steps_total ? step0 + steps_per_block : steps_total;
   if (step0 >= step_end) return;
   const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
-  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+  uint8_t* dp[R];  // all pointers before the first store (see gf_apply_body)
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
   const uint8_t* src[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) src[j] = sp[j];
@@ -363,7 +385,9 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
   if (col >= a.nvec) return;
   const int s = blockIdx.y;
   const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
-  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+  uint8_t* dp[R];  // all pointers before the first store (see gf_apply_body)
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
 
   u32x4 x[K];
 #pragma unroll
@@ -403,7 +427,9 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm_generic(ApplyArgs a) {
   if (col >= a.nvec) return;
   const int s = blockIdx.y;
   const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
-  uint8_t* const* dp = a.dst + int64_t(s) * a.dst_stride + a.row0;
+  uint8_t* dp[R];  // all pointers before the first store (see gf_apply_body)
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
   u32x4 acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};

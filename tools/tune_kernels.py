@@ -97,6 +97,10 @@ def run_layout(args, k, m, S, B, pad):
         for um, uname in ((0, "none"), (1, "col0"), (3, "rs")):
             variants.append((f"enc apply {uname} nt{nt}", 4, 10, 4, 1, um, q_enc, n_enc, src_enc, dst_enc, B, u_enc,
                              z_enc, (k + m) * S * B, nt))
+        variants.append((f"enc apply rs occ8 nt{nt}", 6, 10, 4, 1, 3, q_enc, n_enc, src_enc, dst_enc, B, u_enc,
+                         z_enc, (k + m) * S * B, nt))
+        variants.append((f"enc apply rs stripefast nt{nt}", 5, 10, 4, 1, 3, q_enc, n_enc, src_enc, dst_enc, B, u_enc,
+                         z_enc, (k + m) * S * B, nt))
     variants.append(("enc lds nt1", 2, 10, 4, 1, 0, q_enc, n_enc, src_enc, dst_enc, B, u_enc, z_enc,
                      (k + m) * S * B, 1))
     for name, row in dec_rows.items():
@@ -104,12 +108,21 @@ def run_layout(args, k, m, S, B, pad):
         ud, zd = masks(row)
         variants.append((f"dec1 {name} vec1 allperm nt1", 0, 10, 1, 1, 2, qd, nd, src_dec, dst_dec, B, ud, zd,
                          (k + 1) * S * B, 1))
-        variants.append((f"dec1 {name} apply {'all' if name == 'ones' else 'none'} nt1", 4, 10, 1, 1,
-                         4 if name == "ones" else 0, qd, nd, src_dec, dst_dec, B, ud, zd, (k + 1) * S * B, 1))
+        for var, tag in ((4, ""), (5, " stripefast"), (6, " occ8")):
+            variants.append((f"dec1 {name} apply {'all' if name == 'ones' else 'none'}{tag} nt1", var, 10, 1, 1,
+                             4 if name == "ones" else 0, qd, nd, src_dec, dst_dec, B, ud, zd, (k + 1) * S * B, 1))
         for bps in (32, 64):
             variants.append((f"dec1 {name} stream bps{bps} nt1", 3, 10, 1, bps, 2, qd, nd, src_dec, dst_dec, B, ud,
                              zd, (k + 1) * S * B, 1))
 
+    for flags in range(4):
+        tag = ("stripe" if flags & 1 else "col") + ("/occ8" if flags & 2 else "/occ7")
+        variants.append((f"F enc {tag}", 7, 10, 4, flags, 3, q_enc, n_enc, src_enc, dst_enc, B, u_enc, z_enc,
+                         (k + m) * S * B, 1))
+        qd, nd = tables(dec_rows["ones"])
+        ud, zd = masks(dec_rows["ones"])
+        variants.append((f"F dec1 {tag}", 7, 10, 1, flags, 4, qd, nd, src_dec, dst_dec, B, ud, zd,
+                         (k + 1) * S * B, 1))
     variants = [v for v in variants if args.only in v[0]]
     times = {v[0]: [] for v in variants}
     if True:

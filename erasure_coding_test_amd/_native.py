@@ -71,6 +71,12 @@ SIGNATURES = {
     "ecgpu_plan_launch": (c_int, [c_void_p, c_void_p]),
     "ecgpu_plan_destroy": (None, [c_void_p]),
     "ecgpu_recommended_shard_stride": (c_int64, [c_int64]),
+    "ecgpu_accum_create": (c_void_p, [c_int, c_int64, c_int]),
+    "ecgpu_accum_add": (c_int, [c_void_p, c_void_p, c_int_p]),
+    "ecgpu_accum_read": (c_int, [c_void_p, c_int, c_void_p, c_int64]),
+    "ecgpu_accum_device_ptr": (c_void_p, [c_void_p, c_int]),
+    "ecgpu_accum_reset": (c_int, [c_void_p]),
+    "ecgpu_accum_destroy": (None, [c_void_p]),
     "ecgpu_encode_batch": (c_int, [c_int, c_int, c_int_p, c_int, c_void_pp, c_void_pp, c_int64, c_void_p]),
 }
 

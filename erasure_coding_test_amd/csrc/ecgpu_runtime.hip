@@ -536,6 +536,88 @@ ECGPU_API int ecgpu_plan_launch(ecgpu_plan* p, void* stream) {
 
 ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p) { plan_free(p); }
 
+// ---------------------------------------------------- ECX accumulators ----
+struct ecgpu_accum {
+  int device = 0, m = 0;
+  int64_t size = 0;
+  size_t slot = 0;
+  uint8_t* d_acc = nullptr;  // m slots, each `slot` bytes (4 KiB-skewed stride)
+  std::vector<char> init;
+};
+
+ECGPU_API ecgpu_accum* ecgpu_accum_create(int m, int64_t size, int device) {
+  if (m <= 0 || size < 0) {
+    fail(ECGPU_ERR_ARG, "ecgpu_accum_create: m > 0 and size >= 0 required");
+    return nullptr;
+  }
+  auto* a = new ecgpu_accum();
+  a->device = device < 0 ? current_device() : device;
+  a->m = m;
+  a->size = size;
+  a->slot = size_t(((size + 255) & ~int64_t(255)) + 4096);
+  a->init.assign(size_t(m), 0);
+  DeviceGuard g(a->device);
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&a->d_acc), a->slot * size_t(m));
+  if (e != hipSuccess) {
+    fail(ECGPU_ERR_HIP, std::string("ecgpu_accum_create: ") + hipGetErrorString(e));
+    delete a;
+    return nullptr;
+  }
+  return a;
+}
+
+ECGPU_API char* ecgpu_accum_device_ptr(ecgpu_accum* a, int i) {
+  if (!a || i < 0 || i >= a->m) return nullptr;
+  return reinterpret_cast<char*>(a->d_acc + size_t(i) * a->slot);
+}
+
+ECGPU_API int ecgpu_accum_add(ecgpu_accum* a, const char* block, const int* coefs) {
+  if (!a || !block || !coefs) return fail(ECGPU_ERR_ARG, "ecgpu_accum_add: bad arguments");
+  LinearTracker t;
+  char* src = const_cast<char*>(block);
+  for (int i = 0; i < a->m; ++i) {  // ecx_datanode_main.cpp:699-735, one accumulator at a time
+    const int c = coefs[i] & 0xFF;
+    if (c == 0) continue;
+    char* acc = ecgpu_accum_device_ptr(a, i);
+    if (c == 1) {
+      if (a->init[i])
+        t.xor3(src, acc, acc);
+      else
+        t.copy(acc, src);
+    } else {
+      t.mul(src, c, acc, a->init[i] != 0);
+    }
+  }
+  DeviceGuard g(a->device);
+  const int rc = execute(t.finish(), a->size);
+  if (rc != ECGPU_OK) return rc;
+  for (int i = 0; i < a->m; ++i)
+    if (coefs[i] & 0xFF) a->init[i] = 1;
+  return ECGPU_OK;
+}
+
+ECGPU_API int ecgpu_accum_read(ecgpu_accum* a, int i, char* out, int64_t nbytes) {
+  if (!a || i < 0 || i >= a->m || !out || nbytes < 0 || nbytes > a->size)
+    return fail(ECGPU_ERR_ARG, "ecgpu_accum_read: bad arguments");
+  if (!a->init[i]) return ECGPU_ERR;
+  DeviceGuard g(a->device);
+  ECGPU_HIP(hipMemcpy(out, ecgpu_accum_device_ptr(a, i), size_t(nbytes), hipMemcpyDefault));
+  return ECGPU_OK;
+}
+
+ECGPU_API int ecgpu_accum_reset(ecgpu_accum* a) {
+  if (!a) return fail(ECGPU_ERR_ARG, "ecgpu_accum_reset: null");
+  std::fill(a->init.begin(), a->init.end(), 0);
+  return ECGPU_OK;
+}
+
+ECGPU_API void ecgpu_accum_destroy(ecgpu_accum* a) {
+  if (!a) return;
+  DeviceGuard g(a->device);
+  if (a->d_acc) (void)hipFree(a->d_acc);
+  delete a;
+}
+
 ECGPU_API int ecgpu_encode_batch(int k, int m, const int* matrix, int stripes, const uint8_t* const* data,
                                  uint8_t* const* coding, int64_t size, void* stream) {
   if (k <= 0 || m <= 0 || !matrix) return fail(ECGPU_ERR_ARG, "ecgpu_encode_batch: bad arguments");

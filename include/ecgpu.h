@@ -118,6 +118,22 @@ ECGPU_API int ecgpu_plan_set_kernel(ecgpu_plan* p, int kind, int nontemporal);
 ECGPU_API int ecgpu_plan_launch(ecgpu_plan* p, void* stream);
 ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p);
 
+/* ECX-style incremental parity accumulation (ecx_datanode_main.cpp:680-735)
+ * with the m accumulators resident in HBM.  Source blocks arrive one at a
+ * time (host or device memory); each ecgpu_accum_add is ONE fused launch
+ * that updates all m accumulators with the reference's per-accumulator
+ * first-touch semantics: coefficient 0 leaves an accumulator untouched, 1
+ * copies (first touch) or XORs, anything else multiplies (first touch) or
+ * multiply-XORs.  Only the block crosses PCIe per arrival; parity is read
+ * out once with ecgpu_accum_read.  All calls are synchronous. */
+typedef struct ecgpu_accum ecgpu_accum;
+ECGPU_API ecgpu_accum* ecgpu_accum_create(int m, int64_t size, int device);
+ECGPU_API int ecgpu_accum_add(ecgpu_accum* a, const char* block, const int* coefs /* m */);
+ECGPU_API int ecgpu_accum_read(ecgpu_accum* a, int i, char* out, int64_t nbytes); /* -1 if never touched */
+ECGPU_API char* ecgpu_accum_device_ptr(ecgpu_accum* a, int i);
+ECGPU_API int ecgpu_accum_reset(ecgpu_accum* a);
+ECGPU_API void ecgpu_accum_destroy(ecgpu_accum* a);
+
 /* HBM layout advice for callers that allocate their own shard slabs:
  * the byte distance to put between consecutive shards (and stripes) of
  * `size`-byte shards.  Shards at power-of-two strides send a column's k+m

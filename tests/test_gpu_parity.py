@@ -357,3 +357,41 @@ def test_all_erasure_patterns_rs63_device(ec, gpu):
                 assert ec.jerasure.jerasure_matrix_decode(k, m, 8, M, rko, list(er), b2[:k], b2[k:], size) == 0
                 for a, b in zip(b2, orig):
                     assert torch.equal(a, b), (er, rko)
+
+
+# ------------------------------------------- ECX device accumulators ----
+@pytest.mark.parametrize("k,m,bs,where", [(3, 3, (1 << 20) // 3 + 1, "host"), (3, 3, (1 << 20) // 3, "device"),
+                                          (10, 4, 4 << 20, "device"), (6, 3, 1000, "host")])
+def test_ecx_parity_accumulator(ec, gpu, restatement, k, m, bs, where):
+    # ecx_datanode_main.cpp:680-735: block j of every source arrives in order;
+    # accumulator i gets coefficient matrix[i*k + j] with first-touch init[].
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    blocks = host_shards(36, bs % 97, k, bs)
+    acc = ec.ParityAccumulator(m, bs)
+    for j in range(k):
+        blk = blocks[j] if where == "host" else to_dev([blocks[j]], gpu)[0]
+        acc.add(blk, [M[i * k + j] for i in range(m)])
+    ref = _encode_ref(restatement, k, m, M, blocks, bs)
+    for i in range(m):
+        out = np.zeros(bs, np.uint8)
+        assert acc.read(i, out)
+        assert np.array_equal(out, ref[i][:bs]), i
+    acc.close()
+
+
+def test_ecx_accumulator_zero_coefficients_and_reset(ec, gpu, restatement):
+    k, m, bs = 4, 3, 4099
+    coef = [[0, 0, 0, 0], [1, 0, 7, 1], [0, 29, 1, 142]]  # row 0 never touched
+    blocks = host_shards(37, 0, k, bs)
+    acc = ec.ParityAccumulator(m, bs)
+    for rnd in range(2):  # second round after reset must not see round-1 state
+        for j in range(k):
+            acc.add(blocks[j], [coef[i][j] for i in range(m)])
+        assert not acc.read(0, np.zeros(bs, np.uint8))
+        ref = _encode_ref(restatement, k, m, [c for row in coef for c in row], blocks, bs)
+        for i in (1, 2):
+            out = np.zeros(bs, np.uint8)
+            assert acc.read(i, out)
+            assert np.array_equal(out, ref[i][:bs])
+        acc.reset()
+    acc.close()

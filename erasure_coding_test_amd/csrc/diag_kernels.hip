@@ -68,6 +68,14 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
     if (K == 10 && R == 1)
       fn = mode == 4 ? (occ8 ? &ecgpu::dev::gf_apply_occ8<10, 1, 4> : &ecgpu::dev::gf_apply<10, 1, 4>)
                      : (occ8 ? &ecgpu::dev::gf_apply_occ8<10, 1, 0> : &ecgpu::dev::gf_apply<10, 1, 0>);
+  } else if (variant == 8) {
+    // production gf_apply with VEC columns per lane (vec in {1,2,4}); mode = UnitMask
+    if (K == 10 && R == 4)
+      fn = vec == 1 ? &ecgpu::dev::gf_apply<10, 4, 3, 1>
+                    : vec == 2 ? &ecgpu::dev::gf_apply<10, 4, 3, 2> : &ecgpu::dev::gf_apply<10, 4, 3, 4>;
+    if (K == 10 && R == 1)
+      fn = vec == 1 ? &ecgpu::dev::gf_apply<10, 1, 4, 1>
+                    : vec == 2 ? &ecgpu::dev::gf_apply<10, 1, 4, 2> : &ecgpu::dev::gf_apply<10, 1, 4, 4>;
   } else if (variant == 2) {
     vec = 1;
     if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_lds<10, 4>;
@@ -90,7 +98,7 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
   a.K = K;
   a.R = R;
   a.nt = nt;
-  const long long per_block = 256LL * (variant == 0 || variant == 1 ? vec : 1);
+  const long long per_block = 256LL * (variant == 0 || variant == 1 || variant == 8 ? vec : 1);
   dim3 grid(unsigned((a.nvec + per_block - 1) / per_block), unsigned(stripes));
   if (variant == 3) grid = dim3(unsigned(vec), unsigned(stripes));
   if (variant == 7) {

@@ -214,12 +214,15 @@ __device__ __forceinline__ uint32_t mac_word(uint32_t acc, const u32x4& q, uint3
   return xor3(acc, xor3(perm_lookup(q.x, s0), perm_lookup(q.y, s1), perm_lookup(q.z, s2)), perm_lookup(q.w, s3));
 }
 
-template <int K, int R, int UNITS>
+// Lane l of block b handles the 16-byte columns (b*VEC + v)*256 + l, v < VEC,
+// of every shard of stripe s: all K*VEC loads are issued before any
+// arithmetic, then R*VEC stores.
+template <int K, int R, int UNITS, int VEC>
 __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
   const unsigned cblk = a.stripe_fast ? blockIdx.y : blockIdx.x;
   const int s = a.stripe_fast ? blockIdx.x : blockIdx.y;
-  const int64_t col = int64_t(cblk) * kBlock + threadIdx.x;
-  if (col >= a.nvec) return;
+  const int64_t col0 = int64_t(cblk) * (VEC * kBlock) + threadIdx.x;
+  if (col0 >= a.nvec) return;
   const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
   // Fetch ALL pointers before the first store: a pointer read after a store
   // cannot use the scalar cache (not coherent with vector stores), and the
@@ -228,52 +231,69 @@ __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
 #pragma unroll
   for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
 
-  u32x4 x[K];
-  if (a.nt) {
+  bool live[VEC];
 #pragma unroll
-    for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, 1);
-  } else {
+  for (int v = 0; v < VEC; ++v) live[v] = col0 + v * kBlock < a.nvec;
+  u32x4 x[VEC][K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, 0);
+  for (int v = 0; v < VEC; ++v) {
+    if (!live[v]) continue;
+    if (a.nt) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) x[v][j] = load16(sp[j], col0 + v * kBlock, 1);
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j) x[v][j] = load16(sp[j], col0 + v * kBlock, 0);
+    }
   }
 
-  u32x4 acc[R];
+  u32x4 acc[VEC][R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+  for (int v = 0; v < VEC; ++v)
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[v][r] = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
   for (int j = 0; j < K; ++j) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (is_unit<UNITS>(r, j)) {
-        acc[r] ^= x[j];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v][r] ^= x[v][j];
       } else {
         const u32x4 q = a.qtab[r * K + j];
-        acc[r].x = mac_word(acc[r].x, q, x[j].x);
-        acc[r].y = mac_word(acc[r].y, q, x[j].y);
-        acc[r].z = mac_word(acc[r].z, q, x[j].z);
-        acc[r].w = mac_word(acc[r].w, q, x[j].w);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          acc[v][r].x = mac_word(acc[v][r].x, q, x[v][j].x);
+          acc[v][r].y = mac_word(acc[v][r].y, q, x[v][j].y);
+          acc[v][r].z = mac_word(acc[v][r].z, q, x[v][j].z);
+          acc[v][r].w = mac_word(acc[v][r].w, q, x[v][j].w);
+        }
       }
     }
   }
 
-  if (a.nt) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], 1);
-  } else {
+  for (int v = 0; v < VEC; ++v) {
+    if (!live[v]) continue;
+    if (a.nt) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], 0);
+      for (int r = 0; r < R; ++r) store16(dp[r], col0 + v * kBlock, acc[v][r], 1);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) store16(dp[r], col0 + v * kBlock, acc[v][r], 0);
+    }
   }
 }
 
-template <int K, int R, int UNITS>
+template <int K, int R, int UNITS, int VEC = 1>
 __global__ __launch_bounds__(kBlock) void gf_apply(ApplyArgs a) {
-  gf_apply_body<K, R, UNITS>(a);
+  gf_apply_body<K, R, UNITS, VEC>(a);
 }
 
 // Same body, register budget capped for 8 waves/SIMD (<= 64 VGPRs).
 template <int K, int R, int UNITS>
 __global__ __launch_bounds__(kBlock, 8) void gf_apply_occ8(ApplyArgs a) {
-  gf_apply_body<K, R, UNITS>(a);
+  gf_apply_body<K, R, UNITS, 1>(a);
 }
 
 // ------------------------------------------------------ PERM, streaming ----

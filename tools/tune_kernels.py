@@ -1,6 +1,6 @@
 """A/B the gf_apply kernel variants on the MI355X in ONE process (interleaved
-rounds, median of each), against a streaming-copy reference with the same
-byte volume.  Workload = the bench's: RS(10,4), 4 MiB shards, 24 stripes.
+rounds in a freshly shuffled order each round, median of each), against a
+streaming-copy reference with the same byte volume.  Workload = the bench's: RS(10,4), 4 MiB shards, 24 stripes.
 
     python tools/tune_kernels.py [--rounds 15] [--stripes 24]
 
@@ -123,11 +123,23 @@ def run_layout(args, k, m, S, B, pad):
         ud, zd = masks(dec_rows["ones"])
         variants.append((f"F dec1 {tag}", 7, 10, 1, flags, 4, qd, nd, src_dec, dst_dec, B, ud, zd,
                          (k + 1) * S * B, 1))
+    for vec in (1, 2, 4):
+        variants.append((f"V enc vec{vec}", 8, 10, 4, vec, 3, q_enc, n_enc, src_enc, dst_enc, B, u_enc, z_enc,
+                         (k + m) * S * B, 1))
+        qd, nd = tables(dec_rows["ones"])
+        ud, zd = masks(dec_rows["ones"])
+        variants.append((f"V dec1 vec{vec}", 8, 10, 1, vec, 4, qd, nd, src_dec, dst_dec, B, ud, zd,
+                         (k + 1) * S * B, 1))
     variants = [v for v in variants if args.only in v[0]]
     times = {v[0]: [] for v in variants}
+    import random
+    order = list(variants)
     if True:
         for rnd in range(args.rounds + 2):
-            for v in variants:
+            # shuffled every round: a kernel pays for the dirty lines its
+            # predecessor left behind, so a fixed order biases the medians
+            random.Random(rnd).shuffle(order)
+            for v in order:
                 name, var, K, R, vec, mode, qt, nb, st, dt, stripes, um, zm, nbytes, nt = v
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()

@@ -231,6 +231,46 @@ __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
 #pragma unroll
   for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
 
+  if constexpr (VEC == 1) {
+    // Single column per lane (production): straight-line form, which keeps
+    // the register allocation low (69 VGPRs for RS(10,4)).
+    const int64_t col = col0;
+    u32x4 x[K];
+    if (a.nt) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, 1);
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, 0);
+    }
+    u32x4 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (is_unit<UNITS>(r, j)) {
+          acc[r] ^= x[j];
+        } else {
+          const u32x4 q = a.qtab[r * K + j];
+          acc[r].x = mac_word(acc[r].x, q, x[j].x);
+          acc[r].y = mac_word(acc[r].y, q, x[j].y);
+          acc[r].z = mac_word(acc[r].z, q, x[j].z);
+          acc[r].w = mac_word(acc[r].w, q, x[j].w);
+        }
+      }
+    }
+    if (a.nt) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], 1);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], 0);
+    }
+    return;
+  }
+
   bool live[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) live[v] = col0 + v * kBlock < a.nvec;

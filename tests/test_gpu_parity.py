@@ -395,3 +395,70 @@ def test_ecx_accumulator_zero_coefficients_and_reset(ec, gpu, restatement):
             assert np.array_equal(out, ref[i][:bs])
         acc.reset()
     acc.close()
+
+
+# ------------------------------------------------ concurrency, graphs ----
+def test_concurrent_callers_get_independent_contexts(ec, gpu, restatement):
+    # client_main.cpp:1074-1164 runs ENC_THREAD_NUM encode pthreads at once;
+    # every thread here encodes its own byte range of one stripe, repeatedly.
+    import threading
+    k, m, size, threads = 6, 3, (1 << 20) + 13, 8
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = host_shards(38, 0, k, size)
+    coding = alloc_shards(m, size, PAD)
+    bounds = [(t * size // threads, (t + 1) * size // threads) for t in range(threads)]
+    errors = []
+
+    def work(lo, hi):
+        try:
+            n = hi - lo
+            d = [np.frombuffer((ctypes.c_uint8 * n).from_address(x.ctypes.data + lo), np.uint8) for x in data]
+            c = [np.frombuffer((ctypes.c_uint8 * n).from_address(x.ctypes.data + lo), np.uint8) for x in coding]
+            for _ in range(5):
+                ec.jerasure.jerasure_matrix_encode(k, m, 8, M, d, c, n)
+        except Exception as e:  # pragma: no cover - surfaced below
+            errors.append(e)
+
+    ts = [threading.Thread(target=work, args=b) for b in bounds]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    for a, b in zip(coding, _encode_ref(restatement, k, m, M, data, size)):
+        assert np.array_equal(a[:size], b[:size])
+
+
+def test_plan_launch_is_graph_capturable(ec, gpu, restatement):
+    import torch
+    k, m, size, stripes = 10, 4, 1 << 16, 3
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    slab, shards = ec.alloc_stripes(stripes, k, m, size)
+    slab.zero_()
+    enc = ec.encode_plan(k, m, M).bind([st[:k] for st in shards], [st[k:] for st in shards], size)
+    dec = ec.DecodePlan(k, m, M, [0, 12]).bind_stripes(shards, size)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        enc.launch()  # warm-up outside capture
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        enc.launch()
+        for st in shards:  # erase, then rebuild inside the same graph
+            st[0].fill_(0)
+            st[12].fill_(0)
+        dec.launch()
+    for rnd in range(2):
+        hdata = [host_shards(39, rnd * 10 + st, k, size) for st in range(stripes)]
+        for st in range(stripes):
+            for j in range(k):
+                shards[st][j].copy_(torch.from_numpy(hdata[st][j][:size]))
+        g.replay()
+        torch.cuda.synchronize()
+        for st in range(stripes):
+            ref = _encode_ref(restatement, k, m, M, hdata[st], size)
+            for i in range(m):
+                assert np.array_equal(shards[st][k + i].cpu().numpy(), ref[i][:size]), (rnd, st, i)
+            for j in range(k):
+                assert np.array_equal(shards[st][j].cpu().numpy(), hdata[st][j][:size])

@@ -71,6 +71,13 @@ SIGNATURES = {
     "ecgpu_plan_launch": (c_int, [c_void_p, c_void_p]),
     "ecgpu_plan_destroy": (None, [c_void_p]),
     "ecgpu_recommended_shard_stride": (c_int64, [c_int64]),
+    "ecgpu_pipeline_create": (c_void_p, [c_int, c_int, c_int_p, c_int64, c_int, c_int]),
+    "ecgpu_pipeline_submit": (c_int64, [c_void_p, c_void_pp, c_void_pp]),
+    "ecgpu_pipeline_wait": (c_int, [c_void_p, c_int64]),
+    "ecgpu_pipeline_drain": (c_int, [c_void_p]),
+    "ecgpu_pipeline_destroy": (None, [c_void_p]),
+    "ecgpu_host_register": (c_int, [c_void_p, c_int64]),
+    "ecgpu_host_unregister": (c_int, [c_void_p]),
     "ecgpu_accum_create": (c_void_p, [c_int, c_int64, c_int]),
     "ecgpu_accum_add": (c_int, [c_void_p, c_void_p, c_int_p]),
     "ecgpu_accum_read": (c_int, [c_void_p, c_int, c_void_p, c_int64]),

@@ -618,6 +618,158 @@ ECGPU_API void ecgpu_accum_destroy(ecgpu_accum* a) {
   delete a;
 }
 
+// ---------------------------------------------------- host pipeline ----
+struct ecgpu_pipeline {
+  int device = 0, k = 0, m = 0, depth = 0;
+  int64_t size = 0;
+  size_t slot_stride = 0;  // bytes between shards inside a ring slot
+  uint8_t* d_ring = nullptr;
+  std::vector<ecgpu_plan*> plans;  // one bound plan per ring slot
+  hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
+  std::vector<hipEvent_t> loaded, computed, drained;
+  std::vector<int64_t> slot_ticket;  // ticket occupying each slot (-1: free)
+  int64_t next_ticket = 0;
+  int64_t done_below = 0;             // every ticket < done_below has completed
+  std::mutex mu;
+};
+
+namespace {
+void pipeline_free(ecgpu_pipeline* p) {
+  if (!p) return;
+  DeviceGuard g(p->device);
+  for (auto* pl : p->plans) plan_free(pl);
+  for (auto& v : {&p->loaded, &p->computed, &p->drained})
+    for (auto e : *v)
+      if (e) (void)hipEventDestroy(e);
+  for (auto s : {p->s_h2d, p->s_comp, p->s_d2h})
+    if (s) (void)hipStreamDestroy(s);
+  if (p->d_ring) (void)hipFree(p->d_ring);
+  delete p;
+}
+
+int pipeline_retire(ecgpu_pipeline* p, int slot) {
+  const int64_t t = p->slot_ticket[slot];
+  if (t < 0) return ECGPU_OK;
+  ECGPU_HIP(hipEventSynchronize(p->drained[slot]));
+  p->slot_ticket[slot] = -1;
+  // tickets complete in submission order (the D2H stream is in order)
+  if (t + 1 > p->done_below) p->done_below = t + 1;
+  return ECGPU_OK;
+}
+}  // namespace
+
+ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create(int k, int m, const int* matrix, int64_t size, int depth,
+                                                int device) {
+  if (k <= 0 || m <= 0 || !matrix || size <= 0 || depth <= 0) {
+    fail(ECGPU_ERR_ARG, "ecgpu_pipeline_create: bad arguments");
+    return nullptr;
+  }
+  auto* p = new ecgpu_pipeline();
+  p->device = device < 0 ? current_device() : device;
+  p->k = k;
+  p->m = m;
+  p->depth = depth;
+  p->size = size;
+  p->slot_stride = size_t(ecgpu_recommended_shard_stride(size));
+  DeviceGuard g(p->device);
+  auto bad = [&](hipError_t e, const char* what) {
+    fail(ECGPU_ERR_HIP, std::string("ecgpu_pipeline_create: ") + what + ": " + hipGetErrorString(e));
+    pipeline_free(p);
+    return nullptr;
+  };
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&p->d_ring), p->slot_stride * size_t(k + m) * size_t(depth));
+  if (e != hipSuccess) return bad(e, "hipMalloc");
+  for (hipStream_t* s : {&p->s_h2d, &p->s_comp, &p->s_d2h})
+    if ((e = hipStreamCreateWithFlags(s, hipStreamNonBlocking)) != hipSuccess) return bad(e, "stream");
+  for (auto* v : {&p->loaded, &p->computed, &p->drained}) {
+    v->assign(size_t(depth), nullptr);
+    for (auto& ev : *v)
+      if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "event");
+  }
+  p->slot_ticket.assign(size_t(depth), -1);
+  for (int sl = 0; sl < depth; ++sl) {
+    uint8_t* base = p->d_ring + p->slot_stride * size_t(k + m) * size_t(sl);
+    std::vector<const uint8_t*> src(static_cast<size_t>(k));
+    std::vector<uint8_t*> dst(static_cast<size_t>(m));
+    for (int j = 0; j < k; ++j) src[j] = base + p->slot_stride * size_t(j);
+    for (int i = 0; i < m; ++i) dst[i] = base + p->slot_stride * size_t(k + i);
+    auto* pl = new ecgpu_plan();
+    if (plan_init(pl, m, k, matrix, p->device) != ECGPU_OK ||
+        plan_bind(pl, 1, src.data(), dst.data(), size, nullptr) != ECGPU_OK) {
+      plan_free(pl);
+      pipeline_free(p);
+      return nullptr;
+    }
+    p->plans.push_back(pl);
+  }
+  return p;
+}
+
+ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, char** coding_ptrs) {
+  if (!p || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_submit: bad arguments");
+  std::lock_guard<std::mutex> lk(p->mu);
+  DeviceGuard g(p->device);
+  const int64_t t = p->next_ticket;
+  const int sl = int(t % p->depth);
+  int rc = pipeline_retire(p, sl);  // the slot's previous stripe must be out
+  if (rc != ECGPU_OK) return rc;
+  uint8_t* base = p->d_ring + p->slot_stride * size_t(p->k + p->m) * size_t(sl);
+  for (int j = 0; j < p->k; ++j)
+    ECGPU_HIP(hipMemcpyAsync(base + p->slot_stride * size_t(j), data_ptrs[j], size_t(p->size), hipMemcpyDefault,
+                             p->s_h2d));
+  ECGPU_HIP(hipEventRecord(p->loaded[sl], p->s_h2d));
+  ECGPU_HIP(hipStreamWaitEvent(p->s_comp, p->loaded[sl], 0));
+  rc = plan_launch(p->plans[sl], p->s_comp);
+  if (rc != ECGPU_OK) return rc;
+  ECGPU_HIP(hipEventRecord(p->computed[sl], p->s_comp));
+  ECGPU_HIP(hipStreamWaitEvent(p->s_d2h, p->computed[sl], 0));
+  for (int i = 0; i < p->m; ++i)
+    ECGPU_HIP(hipMemcpyAsync(coding_ptrs[i], base + p->slot_stride * size_t(p->k + i), size_t(p->size),
+                             hipMemcpyDefault, p->s_d2h));
+  ECGPU_HIP(hipEventRecord(p->drained[sl], p->s_d2h));
+  p->slot_ticket[sl] = t;
+  p->next_ticket = t + 1;
+  return t;
+}
+
+ECGPU_API int ecgpu_pipeline_wait(ecgpu_pipeline* p, int64_t ticket) {
+  if (!p || ticket < 0) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_wait: bad arguments");
+  std::lock_guard<std::mutex> lk(p->mu);
+  if (ticket < p->done_below) return ECGPU_OK;
+  if (ticket >= p->next_ticket) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_wait: ticket not submitted");
+  DeviceGuard g(p->device);
+  // retire every slot up to and including the ticket's (completion is in order)
+  for (int64_t t = p->done_below; t <= ticket; ++t) {
+    const int rc = pipeline_retire(p, int(t % p->depth));
+    if (rc != ECGPU_OK) return rc;
+  }
+  return ECGPU_OK;
+}
+
+ECGPU_API int ecgpu_pipeline_drain(ecgpu_pipeline* p) {
+  if (!p) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_drain: null");
+  if (p->next_ticket == 0) return ECGPU_OK;
+  return ecgpu_pipeline_wait(p, p->next_ticket - 1);
+}
+
+ECGPU_API void ecgpu_pipeline_destroy(ecgpu_pipeline* p) {
+  if (!p) return;
+  (void)ecgpu_pipeline_drain(p);
+  pipeline_free(p);
+}
+
+ECGPU_API int ecgpu_host_register(void* ptr, int64_t bytes) {
+  if (!ptr || bytes <= 0) return fail(ECGPU_ERR_ARG, "ecgpu_host_register: bad arguments");
+  ECGPU_HIP(hipHostRegister(ptr, size_t(bytes), hipHostRegisterDefault));
+  return ECGPU_OK;
+}
+
+ECGPU_API int ecgpu_host_unregister(void* ptr) {
+  if (!ptr) return fail(ECGPU_ERR_ARG, "ecgpu_host_unregister: null");
+  ECGPU_HIP(hipHostUnregister(ptr));
+  return ECGPU_OK;
+}
+
 ECGPU_API int ecgpu_encode_batch(int k, int m, const int* matrix, int stripes, const uint8_t* const* data,
                                  uint8_t* const* coding, int64_t size, void* stream) {
   if (k <= 0 || m <= 0 || !matrix) return fail(ECGPU_ERR_ARG, "ecgpu_encode_batch: bad arguments");

@@ -1,0 +1,64 @@
+"""Host-memory stripe pipeline (client write path, client_main.cpp:1714-1815).
+
+``HostPipeline`` encodes stripes whose shards live in host memory with the
+H2D copy, the encode and the D2H copy of consecutive stripes overlapped on
+three HIP streams (ecgpu_pipeline_* in include/ecgpu.h).  ``submit`` returns
+a ticket immediately; the buffers must stay untouched until ``wait(ticket)``.
+Pinned buffers (torch ``pin_memory()`` or :func:`host_register`) get
+asynchronous DMA; pageable ones are staged by HIP.
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+from . import _native as N
+from ._buffers import addr, addrs
+
+
+class HostPipeline:
+    def __init__(self, k: int, m: int, matrix: Sequence[int], size: int, depth: int = 3, device: int = -1):
+        self.k, self.m, self.size = k, m, size
+        self._p = N.lib.ecgpu_pipeline_create(k, m, N.int_array(matrix), size, depth, device)
+        if not self._p:
+            raise N.EcgpuError(f"ecgpu_pipeline_create failed: {N.last_error()}")
+        self._keep = {}  # ticket -> buffers (kept alive until waited)
+
+    def submit(self, data_ptrs, coding_ptrs) -> int:
+        if len(data_ptrs) != self.k or len(coding_ptrs) != self.m:
+            raise ValueError("k data and m coding buffers required")
+        t = N.lib.ecgpu_pipeline_submit(self._p, N.ptr_array(addrs(data_ptrs)), N.ptr_array(addrs(coding_ptrs)))
+        if t < 0:
+            raise N.EcgpuError(f"ecgpu_pipeline_submit failed ({t}): {N.last_error()}")
+        self._keep[t] = (data_ptrs, coding_ptrs)
+        return t
+
+    def wait(self, ticket: int) -> None:
+        N.check(N.lib.ecgpu_pipeline_wait(self._p, ticket), "ecgpu_pipeline_wait")
+        for t in [t for t in self._keep if t <= ticket]:
+            del self._keep[t]
+
+    def drain(self) -> None:
+        N.check(N.lib.ecgpu_pipeline_drain(self._p), "ecgpu_pipeline_drain")
+        self._keep.clear()
+
+    def close(self) -> None:
+        if getattr(self, "_p", None):
+            N.lib.ecgpu_pipeline_destroy(self._p)
+            self._p = None
+            self._keep.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def host_register(buf, nbytes: int = -1) -> None:
+    """Page-lock a host buffer (numpy array) for asynchronous DMA."""
+    n = buf.nbytes if nbytes < 0 else nbytes
+    N.check(N.lib.ecgpu_host_register(addr(buf), n), "ecgpu_host_register")
+
+
+def host_unregister(buf) -> None:
+    N.check(N.lib.ecgpu_host_unregister(addr(buf)), "ecgpu_host_unregister")

@@ -134,6 +134,25 @@ ECGPU_API char* ecgpu_accum_device_ptr(ecgpu_accum* a, int i);
 ECGPU_API int ecgpu_accum_reset(ecgpu_accum* a);
 ECGPU_API void ecgpu_accum_destroy(ecgpu_accum* a);
 
+/* Host-memory stripe pipeline (the client write path, client_main.cpp:
+ * 1714-1815): stripes whose shards live in host memory are encoded with the
+ * H2D copy of stripe i+1, the encode of stripe i and the D2H copy of stripe
+ * i-1 overlapped on three HIP streams over a `depth`-deep ring of device
+ * stripe buffers.  submit returns a ticket at once; the caller's buffers must
+ * stay valid and unmodified until ecgpu_pipeline_wait(ticket) returns, after
+ * which the parity is in coding_ptrs.  Copies are asynchronous DMA for pinned
+ * memory (see ecgpu_host_register) and HIP-staged for pageable memory. */
+typedef struct ecgpu_pipeline ecgpu_pipeline;
+ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create(int k, int m, const int* matrix, int64_t size, int depth,
+                                                int device);
+ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, char** coding_ptrs); /* <0: error */
+ECGPU_API int ecgpu_pipeline_wait(ecgpu_pipeline* p, int64_t ticket);
+ECGPU_API int ecgpu_pipeline_drain(ecgpu_pipeline* p);
+ECGPU_API void ecgpu_pipeline_destroy(ecgpu_pipeline* p);
+/* Page-lock caller memory for asynchronous DMA (hipHostRegister). */
+ECGPU_API int ecgpu_host_register(void* ptr, int64_t bytes);
+ECGPU_API int ecgpu_host_unregister(void* ptr);
+
 /* HBM layout advice for callers that allocate their own shard slabs:
  * the byte distance to put between consecutive shards (and stripes) of
  * `size`-byte shards.  Shards at power-of-two strides send a column's k+m

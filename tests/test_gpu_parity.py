@@ -462,3 +462,35 @@ def test_plan_launch_is_graph_capturable(ec, gpu, restatement):
                 assert np.array_equal(shards[st][k + i].cpu().numpy(), ref[i][:size]), (rnd, st, i)
             for j in range(k):
                 assert np.array_equal(shards[st][j].cpu().numpy(), hdata[st][j][:size])
+
+
+# --------------------------------------------------- host pipeline ----
+@pytest.mark.parametrize("memory", ["pageable", "registered", "torch_pinned"])
+def test_host_pipeline_matches_oracle(ec, gpu, restatement, memory):
+    import torch
+    k, m, size, stripes = 10, 4, (1 << 20) + 3, 7
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = [host_shards(40, s, k, size) for s in range(stripes)]
+    coding = [alloc_shards(m, size, PAD) for _ in range(stripes)]
+    if memory == "registered":
+        for bufs in data + coding:
+            for b in bufs:
+                ec.pipeline.host_register(b)
+    if memory == "torch_pinned":
+        data = [[torch.from_numpy(b).pin_memory() for b in st] for st in data]
+        coding = [[torch.zeros(size + PAD, dtype=torch.uint8).pin_memory() for _ in range(m)] for _ in range(stripes)]
+    p = ec.HostPipeline(k, m, M, size, depth=3)
+    tickets = [p.submit(data[s], coding[s]) for s in range(stripes)]
+    p.wait(tickets[2])
+    p.drain()
+    p.close()
+    for s in range(stripes):
+        hd = [np.asarray(b) if not hasattr(b, "numpy") else b.numpy() for b in data[s]]
+        ref = _encode_ref(restatement, k, m, M, hd, size)
+        for i in range(m):
+            got = coding[s][i].numpy() if hasattr(coding[s][i], "numpy") else coding[s][i]
+            assert np.array_equal(got[:size], ref[i][:size]), (s, i)
+    if memory == "registered":
+        for bufs in data + coding:
+            for b in bufs:
+                ec.pipeline.host_unregister(b)

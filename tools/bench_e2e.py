@@ -7,6 +7,9 @@ originate and terminate in host memory sees, and the other BASELINE configs.
                data shards on a copy stream, encode on the compute stream,
                D2H of the 4 parity shards on a second copy stream; 3-deep
                ring of device stripe buffers so copies overlap compute.
+  e2e_pipeline same stripes through the C-level HostPipeline
+               (ecgpu_pipeline_*): per-shard H2D/D2H on its own streams,
+               pinned and pageable source buffers.
   dropin_pageable  jerasure_matrix_encode / _decode straight on malloc'd
                (pageable) numpy buffers through the C ABI -- the reference
                client's call shape (client_main.cpp:1060, :2118).
@@ -107,6 +110,34 @@ def e2e_pinned(stripes=48, k=10, m=4, S=4 << 20, ring=3):
             "h2d_GBps": round(stripes * k * S / t / 1e9, 1), "parity_ok": ok}
 
 
+def e2e_pipeline(stripes=48, k=10, m=4, S=4 << 20, depth=3, pinned=True):
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    host = torch.empty((stripes, k + m, S), dtype=torch.uint8)
+    if pinned:
+        host = host.pin_memory()
+    host[:, :k].random_(0, 256)
+    p = E.HostPipeline(k, m, M, S, depth=depth)
+
+    def run():
+        for s in range(stripes):
+            p.submit([host[s, j] for j in range(k)], [host[s, k + i] for i in range(m)])
+        p.drain()
+
+    run()
+    t0 = time.perf_counter()
+    run()
+    t = time.perf_counter() - t0
+    p.close()
+    ref = torch.empty((m, S), dtype=torch.uint8, device="cuda")
+    d = host[stripes - 1, :k].cuda()
+    E.encode_plan(k, m, M).bind([[d[j] for j in range(k)]], [[ref[i] for i in range(m)]], S).launch()
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(ref.cpu(), host[stripes - 1, k:]))
+    return {"workload": f"RS(10,4) 4 MiB encode via ecgpu_pipeline, {stripes} stripes "
+                        f"{'pinned' if pinned else 'pageable'} host, depth {depth}",
+            "data_GiBps": round(stripes * k * S / t / GiB, 2), "parity_ok": ok}
+
+
 def dropin_pageable(k=10, m=4, S=4 << 20, reps=5):
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     rng = np.random.default_rng(0)
@@ -164,7 +195,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stripes", type=int, default=48)
     a = ap.parse_args()
-    res = {"pcie": pcie_rates(), "e2e_pinned": e2e_pinned(a.stripes), "dropin_pageable": dropin_pageable(),
+    res = {"pcie": pcie_rates(), "e2e_pinned": e2e_pinned(a.stripes),
+           "e2e_pipeline_pinned": e2e_pipeline(a.stripes), "e2e_pipeline_pageable": e2e_pipeline(a.stripes, pinned=False),
+           "dropin_pageable": dropin_pageable(),
            "device_configs": device_configs()}
     print(json.dumps(res, indent=1))
 

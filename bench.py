@@ -81,7 +81,7 @@ def stripes_for_rank(total: int, rank: int, world: int) -> list:
 
 def load_traffic(workload: str):
     """HBM bytes per encode launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_encode.json, written by profiles/collect_pmc.py), or None."""
+    (profiles/pmc_encode.json, written by profiles/summarize.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_encode.json")
     try:
         with open(p) as f:

@@ -64,6 +64,10 @@ SIGNATURES = {
     "ecgpu_galois_region_xor": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     "ecgpu_reed_sol_r6_encode": (c_int, [c_int, c_int, c_void_pp, c_void_pp, c_int]),
     "ecgpu_reed_sol_galois_w08_region_multby_2": (c_int, [c_void_p, c_int]),
+    "ecgpu_reed_sol_galois_w16_region_multby_2": (c_int, [c_void_p, c_int]),
+    "ecgpu_reed_sol_galois_w32_region_multby_2": (c_int, [c_void_p, c_int]),
+    "ecgpu_galois_w16_region_multiply": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int]),
+    "ecgpu_galois_w32_region_multiply": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int]),
     "ecgpu_jerasure_get_stats": (c_int, [c_double_p]),
     "ecgpu_plan_create": (c_void_p, [c_int, c_int, c_int_p, c_int]),
     "ecgpu_plan_bind": (c_int, [c_void_p, c_int, c_void_pp, c_void_pp, c_int64]),
@@ -72,6 +76,7 @@ SIGNATURES = {
     "ecgpu_plan_destroy": (None, [c_void_p]),
     "ecgpu_recommended_shard_stride": (c_int64, [c_int64]),
     "ecgpu_pipeline_create": (c_void_p, [c_int, c_int, c_int_p, c_int64, c_int, c_int]),
+    "ecgpu_pipeline_create_decode": (c_void_p, [c_int, c_int, c_int, c_int_p, c_int, c_int_p, c_int64, c_int, c_int]),
     "ecgpu_pipeline_submit": (c_int64, [c_void_p, c_void_pp, c_void_pp]),
     "ecgpu_pipeline_wait": (c_int, [c_void_p, c_int64]),
     "ecgpu_pipeline_drain": (c_int, [c_void_p]),

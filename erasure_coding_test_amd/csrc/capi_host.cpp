@@ -61,10 +61,10 @@ ECGPU_API int ecgpu_jerasure_make_decoding_matrix(int k, int m, int w, int* matr
 // then reads the fused map back in terms of ids.
 ECGPU_API int ecgpu_decode_plan(int k, int m, int w, const int* matrix, int row_k_ones, const int* erasures,
                                 int* out_ids, int* n_out, int* src_ids, int* n_src, int* coefs) {
-  if (w != 8 || k <= 0 || m <= 0 || !matrix || !erasures) return ECGPU_ERR_ARG;
+  if ((w != 8 && w != 16 && w != 32) || k <= 0 || m <= 0 || !matrix || !erasures) return ECGPU_ERR_ARG;
   std::vector<char*> ids(size_t(k + m));
   for (int i = 0; i < k + m; ++i) ids[i] = reinterpret_cast<char*>(uintptr_t(i) + 1);
-  LinearTracker t;
+  LinearTracker t(w);
   for (int i = 0; i < k + m; ++i) t.id(ids[i]);
   if (plan_decode(t, k, m, matrix, row_k_ones, erasures, ids.data(), ids.data() + k, 1) < 0) return ECGPU_ERR;
   const FusedOp op = t.finish();

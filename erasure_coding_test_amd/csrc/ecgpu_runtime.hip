@@ -96,7 +96,7 @@ struct Table {
 using SpecTable = Table<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
 
 // Which compile-time unit structure holds exactly for rows [r0, r0+R).
-int unit_variant(const std::vector<uint8_t>& coef, int K, int r0, int R) {
+int unit_variant(const std::vector<uint32_t>& coef, int K, int r0, int R) {
   bool all = true, col0 = true, row0 = true;
   for (int r = 0; r < R; ++r)
     for (int j = 0; j < K; ++j) {
@@ -139,15 +139,50 @@ void build_tables(int c, u32x4* q, uint8_t* nib) {
   }
 }
 
+// Wide-word tables (gf_kernels.hpp, "wide words"): for coefficient c of
+// GF(2^(8W)), the v_perm table pairs of every (rotation d, slice p[, lane
+// pair h]).  lane_table(o, b, p) byte e = byte o of c * ((e << 2p) << 8b).
+void build_wide_tables(uint32_t c, int W, uint32_t* t) {
+  const int w = 8 * W;
+  auto lane_table = [&](int o, int b, int p) {
+    uint32_t v = 0;
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t x = uint32_t(e) << (2 * p) << (8 * b);
+      v |= ((gf_mul_poly(x, c, w) >> (8 * o)) & 0xFFu) << (8 * e);
+    }
+    return v;
+  };
+  if (W == 2) {
+    for (int d = 0; d < 2; ++d)
+      for (int p = 0; p < 4; ++p) {
+        const int i = d * 4 + p;
+        t[2 * i] = lane_table(1, (1 + d) % 2, p);  // odd lanes (selectors 4..7)
+        t[2 * i + 1] = lane_table(0, d % 2, p);    // even lanes (selectors 0..3)
+      }
+  } else {
+    for (int d = 0; d < 4; ++d)
+      for (int p = 0; p < 4; ++p)
+        for (int h = 0; h < 2; ++h) {
+          const int i = (d * 4 + p) * 2 + h, lo = 2 * h, hi = 2 * h + 1;
+          t[2 * i] = lane_table(hi, (hi + d) % 4, p);
+          t[2 * i + 1] = lane_table(lo, (lo + d) % 4, p);
+        }
+  }
+}
+
+int wide_words_per_coef(int w) { return w == 16 ? 2 * dev::Wide<2>::kPerms : 2 * dev::Wide<4>::kPerms; }
+
 }  // namespace
 
 // ----------------------------------------------------------------- plan ----
 struct ecgpu_plan {
-  int device = 0, rows = 0, nsrc = 0;
+  int device = 0, rows = 0, nsrc = 0, w = 8;
   int kind = ECGPU_KERNEL_PERM, nt = 1;
-  std::vector<uint8_t> coef;  // host copy, rows x nsrc
+  std::vector<uint32_t> coef;  // host copy, rows x nsrc
   u32x4* d_q = nullptr;
   uint8_t* d_nib = nullptr;
+  uint32_t* d_w = nullptr;     // wide-word tables (w = 16 / 32)
+  uint8_t* d_wcls = nullptr;   // wide coefficient classes
   int stripes = 0;
   int64_t size = 0;
   bool aligned = true;
@@ -175,20 +210,40 @@ void plan_free(ecgpu_plan* p) {
   DeviceGuard g(p->device);
   if (p->d_q) (void)hipFree(p->d_q);
   if (p->d_nib) (void)hipFree(p->d_nib);
+  if (p->d_w) (void)hipFree(p->d_w);
+  if (p->d_wcls) (void)hipFree(p->d_wcls);
   if (p->d_src) (void)hipFree(p->d_src);
   if (p->d_dst) (void)hipFree(p->d_dst);
   delete p;
 }
 
-int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device) {
+int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, int w = 8) {
   p->device = device;
   p->rows = rows;
   p->nsrc = nsrc;
+  p->w = w;
   p->kind = env_int("ECGPU_KERNEL", ECGPU_KERNEL_PERM);
   p->nt = env_int("ECGPU_NT", 1);
   const size_t n = size_t(rows) * nsrc;
   p->coef.resize(n);
-  for (size_t i = 0; i < n; ++i) p->coef[i] = uint8_t(coefs[i] & 0xFF);
+  if (w != 8) {
+    const uint32_t mask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
+    const int nw = wide_words_per_coef(w);
+    std::vector<uint32_t> t(n * size_t(nw));
+    std::vector<uint8_t> cls(n);
+    for (size_t i = 0; i < n; ++i) {
+      p->coef[i] = uint32_t(coefs[i]) & mask;
+      cls[i] = p->coef[i] == 0 ? 2 : p->coef[i] == 1 ? 1 : 0;
+      build_wide_tables(p->coef[i], w / 8, &t[i * size_t(nw)]);
+    }
+    DeviceGuard g(device);
+    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_w), t.size() * sizeof(uint32_t)));
+    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_wcls), n));
+    ECGPU_HIP(hipMemcpy(p->d_w, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    ECGPU_HIP(hipMemcpy(p->d_wcls, cls.data(), n, hipMemcpyHostToDevice));
+    return ECGPU_OK;
+  }
+  for (size_t i = 0; i < n; ++i) p->coef[i] = uint32_t(coefs[i]) & 0xFFu;
   std::vector<u32x4> q(n);
   std::vector<uint8_t> nib(n * 32);
   for (size_t i = 0; i < n; ++i) build_tables(coefs[i], &q[i], &nib[i * 32]);
@@ -233,9 +288,57 @@ int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* co
   return ECGPU_OK;
 }
 
+// w = 16 / 32: 16-B column kernel over the aligned part, word kernel for the
+// rest; size must be a whole number of words (checked by the callers).
+int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
+  const int K = p->nsrc, W = p->w / 8, nw = wide_words_per_coef(p->w);
+  const int64_t nvec = p->aligned ? p->size / 16 : 0;
+  const int64_t byte0 = nvec * 16;
+  const dim3 block(dev::kBlock);
+  constexpr int kMaxGridY = 65535;
+  for (int r0 = 0; r0 < p->rows; r0 += dev::kMaxRows) {
+    const int R = std::min(dev::kMaxRows, p->rows - r0);
+    KernelFn vec_fn = nullptr, word_fn = W == 2 ? &dev::gf_apply_wide_words<2> : &dev::gf_apply_wide_words<4>;
+    switch (R) {
+      case 1: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 1> : &dev::gf_apply_wide<4, 1>; break;
+      case 2: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 2> : &dev::gf_apply_wide<4, 2>; break;
+      case 3: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 3> : &dev::gf_apply_wide<4, 3>; break;
+      default: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 4> : &dev::gf_apply_wide<4, 4>; break;
+    }
+    for (int s0 = 0; s0 < p->stripes; s0 += kMaxGridY) {
+      const int ns = std::min(kMaxGridY, p->stripes - s0);
+      ApplyArgs a{};
+      a.wtab = p->d_w + size_t(r0) * K * nw;
+      a.wcls = p->d_wcls + size_t(r0) * K;
+      a.src = p->d_src + size_t(s0) * K;
+      a.dst = p->d_dst + size_t(s0) * p->rows;
+      a.nvec = nvec;
+      a.size = p->size;
+      a.byte0 = byte0;
+      a.src_stride = K;
+      a.dst_stride = p->rows;
+      a.row0 = r0;
+      a.K = K;
+      a.R = R;
+      a.nt = p->nt;
+      if (nvec > 0) {
+        const dim3 grid(unsigned((nvec + dev::kBlock - 1) / dev::kBlock), unsigned(ns));
+        ECGPU_HIP(launch(vec_fn, grid, block, a, stream));
+      }
+      const int64_t words = (p->size - byte0) / W;
+      if (words > 0) {
+        const dim3 grid(unsigned((words + dev::kBlock - 1) / dev::kBlock), unsigned(ns));
+        ECGPU_HIP(launch(word_fn, grid, block, a, stream));
+      }
+    }
+  }
+  return ECGPU_OK;
+}
+
 int plan_launch(ecgpu_plan* p, hipStream_t stream) {
   if (p->stripes <= 0 || p->size <= 0 || p->rows <= 0) return ECGPU_OK;
   DeviceGuard g(p->device);
+  if (p->w != 8) return plan_launch_wide(p, stream);
   const int K = p->nsrc;
   const int64_t nvec = p->aligned ? p->size / 16 : 0;
   const int64_t byte0 = nvec * 16;
@@ -251,7 +354,7 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
     if (spec)
       for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) {
-          const uint8_t c = p->coef[size_t(r0 + r) * K + j];
+          const uint32_t c = p->coef[size_t(r0 + r) * K + j];
           if (c == 1) unit |= uint64_t(1) << (r * K + j);
           if (c == 0) zero |= uint64_t(1) << (r * K + j);
         }
@@ -289,9 +392,9 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
 
 // ------------------------------------------------------ context pool ----
 struct PlanKey {
-  int rows, nsrc;
-  std::vector<uint8_t> coef;
-  bool operator==(const PlanKey& o) const { return rows == o.rows && nsrc == o.nsrc && coef == o.coef; }
+  int rows, nsrc, w;
+  std::vector<uint32_t> coef;
+  bool operator==(const PlanKey& o) const { return rows == o.rows && nsrc == o.nsrc && w == o.w && coef == o.coef; }
 };
 
 struct Ctx {
@@ -343,16 +446,16 @@ void release_ctx(Ctx* c) {
 }
 
 struct CtxLease {
+  int rc = ECGPU_OK;  // declared first: initialised before acquire_ctx writes it
   Ctx* c = nullptr;
-  int rc = ECGPU_OK;
   explicit CtxLease(int device) : c(acquire_ctx(device, &rc)) {}
   ~CtxLease() {
     if (c) release_ctx(c);
   }
 };
 
-int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint8_t>& coef, ecgpu_plan** out) {
-  PlanKey key{rows, nsrc, coef};
+int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int w, ecgpu_plan** out) {
+  PlanKey key{rows, nsrc, w, coef};
   for (auto it = c->plans.begin(); it != c->plans.end(); ++it)
     if (it->first == key) {
       c->plans.splice(c->plans.begin(), c->plans, it);
@@ -361,7 +464,7 @@ int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint8_t>& coef, ecgpu
     }
   auto* p = new ecgpu_plan();
   std::vector<int> ci(coef.begin(), coef.end());
-  int rc = plan_init(p, rows, nsrc, ci.data(), c->device);
+  int rc = plan_init(p, rows, nsrc, ci.data(), c->device, w);
   if (rc != ECGPU_OK) {
     plan_free(p);
     return rc;
@@ -420,6 +523,8 @@ void add_stats(const FusedOp& op) {
 
 // Runs a fused op synchronously over `size` bytes of every buffer.
 int execute(const FusedOp& op, int64_t size) {
+  if (op.w != 8 && size % (op.w / 8) != 0)
+    return fail(ECGPU_ERR_ARG, "w = " + std::to_string(op.w) + ": size must be a multiple of the word size");
   add_stats(op);
   if (op.dsts.empty() || size <= 0) return ECGPU_OK;
   const int device = current_device();
@@ -474,7 +579,7 @@ int execute(const FusedOp& op, int64_t size) {
     for (int r = 0; r < rows; ++r) ECGPU_HIP(hipMemsetAsync(dp[r], 0, size_t(size), c->stream));
   } else {
     ecgpu_plan* p = nullptr;
-    rc = ctx_plan(c, rows, nsrc, op.coef, &p);
+    rc = ctx_plan(c, rows, nsrc, op.coef, op.w, &p);
     if (rc != ECGPU_OK) return rc;
     rc = plan_bind(p, 1, sp.data(), dp.data(), size, c->stream);
     if (rc != ECGPU_OK) return rc;
@@ -622,15 +727,22 @@ ECGPU_API void ecgpu_accum_destroy(ecgpu_accum* a) {
 struct ecgpu_pipeline {
   int device = 0, k = 0, m = 0, depth = 0;
   int64_t size = 0;
-  size_t slot_stride = 0;  // bytes between shards inside a ring slot
-  uint8_t* d_ring = nullptr;
-  std::vector<ecgpu_plan*> plans;  // one bound plan per ring slot
+  std::vector<int> src_ids, out_ids;  // shard ids read / written (id < k: data_ptrs[id], else coding_ptrs[id-k])
+  size_t slot_stride = 0;             // bytes between shards inside a ring slot
+  uint8_t* d_ring = nullptr;          // depth slots x (nsrc inputs, then rows outputs)
+  std::vector<ecgpu_plan*> plans;     // one bound plan per ring slot (none when nsrc or rows is 0)
   hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
   std::vector<hipEvent_t> loaded, computed, drained;
   std::vector<int64_t> slot_ticket;  // ticket occupying each slot (-1: free)
   int64_t next_ticket = 0;
   int64_t done_below = 0;             // every ticket < done_below has completed
   std::mutex mu;
+
+  int nsrc() const { return int(src_ids.size()); }
+  int rows() const { return int(out_ids.size()); }
+  uint8_t* slot_shard(int slot, int j) const {
+    return d_ring + slot_stride * (size_t(nsrc() + rows()) * size_t(slot) + size_t(j));
+  }
 };
 
 namespace {
@@ -656,29 +768,28 @@ int pipeline_retire(ecgpu_pipeline* p, int slot) {
   if (t + 1 > p->done_below) p->done_below = t + 1;
   return ECGPU_OK;
 }
-}  // namespace
 
-ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create(int k, int m, const int* matrix, int64_t size, int depth,
-                                                int device) {
-  if (k <= 0 || m <= 0 || !matrix || size <= 0 || depth <= 0) {
-    fail(ECGPU_ERR_ARG, "ecgpu_pipeline_create: bad arguments");
-    return nullptr;
-  }
+// rows x nsrc coefficient map from shard ids src_ids to shard ids out_ids.
+ecgpu_pipeline* pipeline_build(int k, int m, int rows, int nsrc, const int* coef, const int* src_ids,
+                               const int* out_ids, int64_t size, int depth, int device) {
   auto* p = new ecgpu_pipeline();
   p->device = device < 0 ? current_device() : device;
   p->k = k;
   p->m = m;
   p->depth = depth;
   p->size = size;
+  p->src_ids.assign(src_ids, src_ids + nsrc);
+  p->out_ids.assign(out_ids, out_ids + rows);
   p->slot_stride = size_t(ecgpu_recommended_shard_stride(size));
   DeviceGuard g(p->device);
   auto bad = [&](hipError_t e, const char* what) {
-    fail(ECGPU_ERR_HIP, std::string("ecgpu_pipeline_create: ") + what + ": " + hipGetErrorString(e));
+    fail(ECGPU_ERR_HIP, std::string("ecgpu_pipeline: ") + what + ": " + hipGetErrorString(e));
     pipeline_free(p);
-    return nullptr;
+    return static_cast<ecgpu_pipeline*>(nullptr);
   };
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(&p->d_ring), p->slot_stride * size_t(k + m) * size_t(depth));
-  if (e != hipSuccess) return bad(e, "hipMalloc");
+  hipError_t e = hipSuccess;
+  const size_t ring = p->slot_stride * size_t(nsrc + rows) * size_t(depth);
+  if (ring && (e = hipMalloc(reinterpret_cast<void**>(&p->d_ring), ring)) != hipSuccess) return bad(e, "hipMalloc");
   for (hipStream_t* s : {&p->s_h2d, &p->s_comp, &p->s_d2h})
     if ((e = hipStreamCreateWithFlags(s, hipStreamNonBlocking)) != hipSuccess) return bad(e, "stream");
   for (auto* v : {&p->loaded, &p->computed, &p->drained}) {
@@ -687,45 +798,82 @@ ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create(int k, int m, const int* matrix,
       if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "event");
   }
   p->slot_ticket.assign(size_t(depth), -1);
-  for (int sl = 0; sl < depth; ++sl) {
-    uint8_t* base = p->d_ring + p->slot_stride * size_t(k + m) * size_t(sl);
-    std::vector<const uint8_t*> src(static_cast<size_t>(k));
-    std::vector<uint8_t*> dst(static_cast<size_t>(m));
-    for (int j = 0; j < k; ++j) src[j] = base + p->slot_stride * size_t(j);
-    for (int i = 0; i < m; ++i) dst[i] = base + p->slot_stride * size_t(k + i);
-    auto* pl = new ecgpu_plan();
-    if (plan_init(pl, m, k, matrix, p->device) != ECGPU_OK ||
-        plan_bind(pl, 1, src.data(), dst.data(), size, nullptr) != ECGPU_OK) {
-      plan_free(pl);
-      pipeline_free(p);
-      return nullptr;
+  if (nsrc > 0 && rows > 0) {
+    for (int sl = 0; sl < depth; ++sl) {
+      std::vector<const uint8_t*> src(static_cast<size_t>(nsrc));
+      std::vector<uint8_t*> dst(static_cast<size_t>(rows));
+      for (int j = 0; j < nsrc; ++j) src[j] = p->slot_shard(sl, j);
+      for (int i = 0; i < rows; ++i) dst[i] = p->slot_shard(sl, nsrc + i);
+      auto* pl = new ecgpu_plan();
+      if (plan_init(pl, rows, nsrc, coef, p->device) != ECGPU_OK ||
+          plan_bind(pl, 1, src.data(), dst.data(), size, nullptr) != ECGPU_OK) {
+        plan_free(pl);
+        pipeline_free(p);
+        return nullptr;
+      }
+      p->plans.push_back(pl);
     }
-    p->plans.push_back(pl);
   }
   return p;
+}
+}  // namespace
+
+ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create(int k, int m, const int* matrix, int64_t size, int depth,
+                                                int device) {
+  if (k <= 0 || m <= 0 || !matrix || size <= 0 || depth <= 0) {
+    fail(ECGPU_ERR_ARG, "ecgpu_pipeline_create: bad arguments");
+    return nullptr;
+  }
+  std::vector<int> src(static_cast<size_t>(k)), out(static_cast<size_t>(m));
+  for (int j = 0; j < k; ++j) src[j] = j;
+  for (int i = 0; i < m; ++i) out[i] = k + i;
+  return pipeline_build(k, m, m, k, matrix, src.data(), out.data(), size, depth, device);
+}
+
+ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create_decode(int k, int m, int w, const int* matrix, int row_k_ones,
+                                                       const int* erasures, int64_t size, int depth, int device) {
+  if (k <= 0 || m <= 0 || w != 8 || !matrix || !erasures || size <= 0 || depth <= 0) {
+    fail(ECGPU_ERR_ARG, "ecgpu_pipeline_create_decode: bad arguments");
+    return nullptr;
+  }
+  const size_t n = size_t(k + m);
+  std::vector<int> out(n), src(n), coef(n * n);
+  int n_out = 0, n_src = 0;
+  if (ecgpu_decode_plan(k, m, w, matrix, row_k_ones, erasures, out.data(), &n_out, src.data(), &n_src,
+                        coef.data()) != ECGPU_OK) {
+    fail(ECGPU_ERR, "ecgpu_pipeline_create_decode: erasure pattern not decodable (reference decode returns -1)");
+    return nullptr;
+  }
+  return pipeline_build(k, m, n_out, n_src, coef.data(), src.data(), out.data(), size, depth, device);
 }
 
 ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, char** coding_ptrs) {
   if (!p || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_submit: bad arguments");
   std::lock_guard<std::mutex> lk(p->mu);
   DeviceGuard g(p->device);
+  auto host = [&](int id) { return id < p->k ? data_ptrs[id] : coding_ptrs[id - p->k]; };
   const int64_t t = p->next_ticket;
   const int sl = int(t % p->depth);
   int rc = pipeline_retire(p, sl);  // the slot's previous stripe must be out
   if (rc != ECGPU_OK) return rc;
-  uint8_t* base = p->d_ring + p->slot_stride * size_t(p->k + p->m) * size_t(sl);
-  for (int j = 0; j < p->k; ++j)
-    ECGPU_HIP(hipMemcpyAsync(base + p->slot_stride * size_t(j), data_ptrs[j], size_t(p->size), hipMemcpyDefault,
-                             p->s_h2d));
+  const int ns = p->nsrc(), nr = p->rows();
+  const size_t bytes = size_t(p->size);
+  if (nr > 0)  // nothing to read when no shard is written
+    for (int j = 0; j < ns; ++j)
+      ECGPU_HIP(hipMemcpyAsync(p->slot_shard(sl, j), host(p->src_ids[j]), bytes, hipMemcpyDefault, p->s_h2d));
   ECGPU_HIP(hipEventRecord(p->loaded[sl], p->s_h2d));
   ECGPU_HIP(hipStreamWaitEvent(p->s_comp, p->loaded[sl], 0));
-  rc = plan_launch(p->plans[sl], p->s_comp);
-  if (rc != ECGPU_OK) return rc;
+  if (ns > 0 && nr > 0) {
+    rc = plan_launch(p->plans[sl], p->s_comp);
+    if (rc != ECGPU_OK) return rc;
+  } else {
+    for (int i = 0; i < nr; ++i)  // rows with no source: all-zero output
+      ECGPU_HIP(hipMemsetAsync(p->slot_shard(sl, ns + i), 0, bytes, p->s_comp));
+  }
   ECGPU_HIP(hipEventRecord(p->computed[sl], p->s_comp));
   ECGPU_HIP(hipStreamWaitEvent(p->s_d2h, p->computed[sl], 0));
-  for (int i = 0; i < p->m; ++i)
-    ECGPU_HIP(hipMemcpyAsync(coding_ptrs[i], base + p->slot_stride * size_t(p->k + i), size_t(p->size),
-                             hipMemcpyDefault, p->s_d2h));
+  for (int i = 0; i < nr; ++i)
+    ECGPU_HIP(hipMemcpyAsync(host(p->out_ids[i]), p->slot_shard(sl, ns + i), bytes, hipMemcpyDefault, p->s_d2h));
   ECGPU_HIP(hipEventRecord(p->drained[sl], p->s_d2h));
   p->slot_ticket[sl] = t;
   p->next_ticket = t + 1;
@@ -788,26 +936,30 @@ ECGPU_API int ecgpu_encode_batch(int k, int m, const int* matrix, int stripes, c
   return rc;
 }
 
+namespace {
+bool valid_w(int w) { return w == 8 || w == 16 || w == 32; }
+}  // namespace
+
 ECGPU_API int ecgpu_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs,
                                            int size) {
-  if (w != 8) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_encode: w must be 8");
-  LinearTracker t;
+  if (!valid_w(w)) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_encode: w must be 8, 16 or 32");
+  LinearTracker t(w);
   plan_encode(t, k, m, matrix, data_ptrs, coding_ptrs, size);
   return execute(t.finish(), size);
 }
 
 ECGPU_API int ecgpu_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures,
                                            char** data_ptrs, char** coding_ptrs, int size) {
-  if (w != 8) return w == 16 || w == 32 ? fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_decode: w must be 8") : -1;
-  LinearTracker t;
+  if (!valid_w(w)) return ECGPU_ERR;  // jerasure.cpp:165: any other w returns -1
+  LinearTracker t(w);
   if (plan_decode(t, k, m, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size) < 0) return ECGPU_ERR;
   return execute(t.finish(), size);
 }
 
 ECGPU_API int ecgpu_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int dest_id,
                                             char** data_ptrs, char** coding_ptrs, int size) {
-  if (w != 8) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_dotprod: w must be 8");
-  LinearTracker t;
+  if (!valid_w(w)) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_dotprod: w must be 8, 16 or 32");
+  LinearTracker t(w);
   t.dotprod(k, matrix_row, src_ids, dest_id, data_ptrs, coding_ptrs, size);
   return execute(t.finish(), size);
 }
@@ -829,6 +981,26 @@ ECGPU_API int ecgpu_galois_w08_region_multiply(char* region, int multby, int nby
   return execute(t.finish(), nbytes);
 }
 
+// galois.cpp:469-542: nbytes/2 words; multby 0 zeroes (no add) or does
+// nothing (add); in place (r2 NULL) ignores add.
+ECGPU_API int ecgpu_galois_w16_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
+  LinearTracker t(16);
+  char* dst = r2 ? r2 : region;
+  if (multby == 0) {
+    if (!add) t.mul(region, 0, dst, false);
+  } else {
+    t.mul(region, multby, dst, r2 != nullptr && add != 0);
+  }
+  return execute(t.finish(), nbytes & ~1);
+}
+
+// galois.cpp:666-727: nbytes/4 words; add applies even in place.
+ECGPU_API int ecgpu_galois_w32_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
+  LinearTracker t(32);
+  t.mul(region, multby, r2 ? r2 : region, add != 0);
+  return execute(t.finish(), nbytes & ~3);
+}
+
 ECGPU_API int ecgpu_galois_region_xor(char* r1, char* r2, char* r3, int nbytes) {
   LinearTracker t;
   t.xor3(r1, r2, r3);
@@ -841,10 +1013,24 @@ ECGPU_API int ecgpu_reed_sol_galois_w08_region_multby_2(char* region, int nbytes
   return execute(t.finish(), nbytes);
 }
 
-// reed_sol.cpp:200-225 (w = 8): P = XOR of data; Q = Horner sum of 2^j d_j.
+// reed_sol.cpp:158-198 / :90-106 (whole words).
+ECGPU_API int ecgpu_reed_sol_galois_w16_region_multby_2(char* region, int nbytes) {
+  LinearTracker t(16);
+  t.mul(region, 2, region, false);
+  return execute(t.finish(), nbytes & ~1);
+}
+
+ECGPU_API int ecgpu_reed_sol_galois_w32_region_multby_2(char* region, int nbytes) {
+  LinearTracker t(32);
+  t.mul(region, 2, region, false);
+  return execute(t.finish(), nbytes & ~3);
+}
+
+// reed_sol.cpp:200-225: P = XOR of data; Q = Horner sum of 2^j d_j.
+// Returns 1, or 0 for a w the reference does not handle.
 ECGPU_API int ecgpu_reed_sol_r6_encode(int k, int w, char** data_ptrs, char** coding_ptrs, int size) {
-  if (w != 8) return fail(ECGPU_ERR_ARG, "ecgpu_reed_sol_r6_encode: w must be 8");
-  LinearTracker t;
+  if (!valid_w(w)) return 0;
+  LinearTracker t(w);
   t.copy(coding_ptrs[0], data_ptrs[0]);
   for (int i = 1; i < k; ++i) t.xor3(coding_ptrs[0], data_ptrs[i], coding_ptrs[0]);
   t.copy(coding_ptrs[1], data_ptrs[k - 1]);

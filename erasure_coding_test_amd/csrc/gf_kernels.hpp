@@ -51,6 +51,8 @@ struct ApplyArgs {
   int K, R;                       // runtime copies (generic / byte kernels)
   int nt;                         // 1: non-temporal loads/stores
   int stripe_fast;                // 1: blockIdx.x = stripe, blockIdx.y = column block
+  const uint32_t* wtab;           // [R][K][2 * Wide<W>::kPerms] wide-word tables (w = 16 / 32)
+  const uint8_t* wcls;            // [R][K] wide coefficient class: 0 general, 1 unit, 2 zero
 };
 
 // How a launch treats coefficients 0 and 1.
@@ -549,6 +551,133 @@ __global__ __launch_bounds__(kBlock) void gf_apply_bytes(ApplyArgs a) {
     for (int r = 0; r < a.R; ++r) acc[r] ^= gf_mul_perm(a.qtab[r * a.K + j], s0, s1, s2, s3);
   }
   for (int r = 0; r < a.R; ++r) dp[r][x] = uint8_t(acc[r]);
+}
+
+
+// ------------------------------------------- wide words (w = 16 and 32) ----
+// jerasure.h's w = 16 / 32 surface (galois.cpp:469-729).  c*x in GF(2^16) or
+// GF(2^32) is GF(2)-linear in x, so output byte o of c*x is the XOR over
+// input bytes b of a byte->byte linear map L_{b->o}, and every such map
+// splits into four 2-bit-slice lookups exactly as at w = 8.  Rotating the
+// word by d bytes puts input byte b = (o + d) mod W under output lane o, so
+// ONE v_perm per (rotation, slice) serves every lane whose table differs only
+// by lane class:
+//   w = 16 (W = 2): lane classes even / odd -> table A in the low dword of
+//     the v_perm pool (selectors 0..3), B in the high dword (4..7):
+//     2 rotations x 4 slices = 8 v_perm per coefficient-dword;
+//   w = 32 (W = 4): four lane classes -> two v_perm per (rotation, slice),
+//     each zeroing the other lane pair with selector 0x0C:
+//     4 x 4 x 2 = 32 v_perm per coefficient-dword.
+// Table word pairs per v_perm: [2i] = pool high dword (B), [2i+1] = low (A).
+template <int W>
+struct Wide;
+template <>
+struct Wide<2> {
+  static constexpr int kPerms = 8;
+};
+template <>
+struct Wide<4> {
+  static constexpr int kPerms = 32;
+};
+
+template <int W>
+__device__ __forceinline__ void wide_sel(uint32_t x, uint32_t (&sel)[Wide<W>::kPerms]) {
+  if constexpr (W == 2) {
+    const uint32_t xs = __builtin_amdgcn_perm(x, x, 0x02030001u);  // swap the bytes of each 16-bit word
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      sel[p] = ((x >> (2 * p)) & kLo2) | 0x04000400u;
+      sel[4 + p] = ((xs >> (2 * p)) & kLo2) | 0x04000400u;
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t xr = d == 0 ? x : __builtin_amdgcn_alignbit(x, x, 8 * d);  // rotr(x, 8d)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const uint32_t t = (xr >> (2 * p)) & kLo2;
+        sel[(d * 4 + p) * 2 + 0] = (t & 0x00000303u) | 0x0C0C0400u;
+        sel[(d * 4 + p) * 2 + 1] = (t & 0x03030000u) | 0x04000C0Cu;
+      }
+    }
+  }
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t wide_mac(uint32_t acc, const uint32_t* __restrict__ t,
+                                             const uint32_t (&sel)[Wide<W>::kPerms]) {
+#pragma unroll
+  for (int i = 0; i < Wide<W>::kPerms; i += 2)
+    acc = xor3(acc, __builtin_amdgcn_perm(t[2 * i], t[2 * i + 1], sel[i]),
+               __builtin_amdgcn_perm(t[2 * i + 2], t[2 * i + 3], sel[i + 1]));
+  return acc;
+}
+
+// 16-byte columns: lane l of block b handles column b*256 + l of every shard
+// of stripe blockIdx.y; runtime K (the w = 16/32 surface is not the hot path).
+template <int W, int R>
+__global__ __launch_bounds__(kBlock) void gf_apply_wide(ApplyArgs a) {
+  const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  constexpr int kWords = 2 * Wide<W>::kPerms;
+  u32x4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+  for (int j = 0; j < a.K; ++j) {
+    const u32x4 x = load16(sp[j], col, a.nt);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint32_t sel[Wide<W>::kPerms];
+      wide_sel<W>(x[c], sel);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint8_t cls = a.wcls[r * a.K + j];
+        if (cls == 2) continue;
+        if (cls == 1) {
+          acc[r][c] ^= x[c];
+          continue;
+        }
+        acc[r][c] = wide_mac<W>(acc[r][c], a.wtab + size_t(r * a.K + j) * kWords, sel);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], a.nt);
+}
+
+// Words from byte0 to size (tails, or whole regions whose pointers are not
+// 16-B aligned): one W-byte word per lane, byte loads and stores.
+template <int W>
+__global__ __launch_bounds__(kBlock) void gf_apply_wide_words(ApplyArgs a) {
+  const int64_t x0 = a.byte0 + (int64_t(blockIdx.x) * kBlock + threadIdx.x) * W;
+  if (x0 + W > a.size) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  constexpr int kWords = 2 * Wide<W>::kPerms;
+  uint32_t acc[kMaxRows] = {0u, 0u, 0u, 0u};
+  for (int j = 0; j < a.K; ++j) {
+    const uint8_t* q = sp[j] + x0;
+    uint32_t x = 0;
+#pragma unroll
+    for (int b = 0; b < W; ++b) x |= uint32_t(q[b]) << (8 * b);
+    uint32_t sel[Wide<W>::kPerms];
+    wide_sel<W>(x, sel);
+    for (int r = 0; r < a.R; ++r) {
+      const uint8_t cls = a.wcls[r * a.K + j];
+      if (cls == 2) continue;
+      acc[r] = cls == 1 ? (acc[r] ^ x) : wide_mac<W>(acc[r], a.wtab + size_t(r * a.K + j) * kWords, sel);
+    }
+  }
+  for (int r = 0; r < a.R; ++r) {
+    uint8_t* d = a.dst[int64_t(s) * a.dst_stride + a.row0 + r] + x0;
+#pragma unroll
+    for (int b = 0; b < W; ++b) d[b] = uint8_t(acc[r] >> (8 * b));
+  }
 }
 
 }  // namespace dev

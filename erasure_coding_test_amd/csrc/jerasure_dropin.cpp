@@ -7,10 +7,13 @@
 // place of src/erasure_coding/*.cpp.  The w = 8 hot path -- matrix encode,
 // decode, dot product, region multiply / XOR, parity, RAID-6 -- runs on the
 // MI355X through include/ecgpu.h; a GPU failure is fatal (message + abort),
-// never a silent CPU fallback.  Host-side math (fields, matrices) comes from
-// libecgpu's host C ABI.  The surface the north star does not cover (w = 16
-// / 32 regions, bit-matrix / schedule coding) is CPU code in
-// jerasure_surface.cpp.
+// never a silent CPU fallback.  The w = 16 / 32 region and matrix calls run
+// on the MI355X too (wide-word kernels) when the size is a whole number of
+// words -- the reference's own precondition (jerasure.h: size a multiple of
+// sizeof(long)); a ragged size, where the reference reads and writes past the
+// region, takes the exact-word CPU restatement in jerasure_surface.cpp.
+// Host-side math (fields, matrices) comes from libecgpu's host C ABI.
+// Bit-matrix / schedule coding is CPU code in jerasure_surface.cpp.
 #include <cstdio>
 #include <cstdlib>
 
@@ -34,6 +37,9 @@ namespace {
 inline void check(const char* fn, int rc) {
   if (rc != ECGPU_OK) gpu_fatal(fn, rc);
 }
+
+// w = 8 always runs on the GPU; w = 16 / 32 when size is whole words.
+inline bool whole_words(int w, int size) { return w == 8 || ((w == 16 || w == 32) && size % (w / 8) == 0); }
 
 }  // namespace
 
@@ -89,11 +95,11 @@ void galois_w08_region_multiply(char* region, int multby, int nbytes, char* r2, 
 }
 
 void galois_w16_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
-  ecgpu_cpu::region_multiply_w16(region, multby, nbytes, r2, add);
+  check("galois_w16_region_multiply", ecgpu_galois_w16_region_multiply(region, multby, nbytes, r2, add));
 }
 
 void galois_w32_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
-  ecgpu_cpu::region_multiply_w32(region, multby, nbytes, r2, add);
+  check("galois_w32_region_multiply", ecgpu_galois_w32_region_multiply(region, multby, nbytes, r2, add));
 }
 
 // ========================================================== reed_sol.h ====
@@ -107,22 +113,21 @@ int* reed_sol_big_vandermonde_distribution_matrix(int rows, int cols, int w) {
 int* reed_sol_r6_coding_matrix(int k, int w) { return ecgpu_reed_sol_r6_coding_matrix(k, w); }
 
 int reed_sol_r6_encode(int k, int w, char** data_ptrs, char** coding_ptrs, int size) {
-  if (w == 8) {
-    const int rc = ecgpu_reed_sol_r6_encode(k, w, data_ptrs, coding_ptrs, size);
-    if (rc < 0) gpu_fatal("reed_sol_r6_encode", rc);
-    return rc;
-  }
-  return ecgpu_cpu::r6_encode(k, w, data_ptrs, coding_ptrs, size);
+  if (w != 8 && w != 16 && w != 32) return 0;
+  if (!whole_words(w, size)) return ecgpu_cpu::r6_encode(k, w, data_ptrs, coding_ptrs, size);
+  const int rc = ecgpu_reed_sol_r6_encode(k, w, data_ptrs, coding_ptrs, size);
+  if (rc < 0) gpu_fatal("reed_sol_r6_encode", rc);
+  return rc;
 }
 
 void reed_sol_galois_w08_region_multby_2(char* region, int nbytes) {
   check("reed_sol_galois_w08_region_multby_2", ecgpu_reed_sol_galois_w08_region_multby_2(region, nbytes));
 }
 void reed_sol_galois_w16_region_multby_2(char* region, int nbytes) {
-  ecgpu_cpu::region_multiply_w16(region, 2, nbytes, nullptr, 0);
+  check("reed_sol_galois_w16_region_multby_2", ecgpu_reed_sol_galois_w16_region_multby_2(region, nbytes));
 }
 void reed_sol_galois_w32_region_multby_2(char* region, int nbytes) {
-  ecgpu_cpu::region_multiply_w32(region, 2, nbytes, nullptr, 0);
+  check("reed_sol_galois_w32_region_multby_2", ecgpu_reed_sol_galois_w32_region_multby_2(region, nbytes));
 }
 
 // ========================================================== jerasure.h ====
@@ -131,7 +136,7 @@ void jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, 
     std::fprintf(stderr, "ERROR: jerasure_matrix_encode() and w is not 8, 16 or 32\n");
     std::exit(1);
   }
-  if (w == 8) {
+  if (whole_words(w, size)) {
     check("jerasure_matrix_encode", ecgpu_jerasure_matrix_encode(k, m, w, matrix, data_ptrs, coding_ptrs, size));
     return;
   }
@@ -142,7 +147,8 @@ void jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, 
 int jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
                            char** coding_ptrs, int size) {
   if (w != 8 && w != 16 && w != 32) return -1;
-  if (w != 8) return ecgpu_cpu::matrix_decode(k, m, w, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size);
+  if (!whole_words(w, size))
+    return ecgpu_cpu::matrix_decode(k, m, w, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size);
   const int rc = ecgpu_jerasure_matrix_decode(k, m, w, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size);
   if (rc == ECGPU_ERR) return -1;
   check("jerasure_matrix_decode", rc);
@@ -155,7 +161,7 @@ void jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int de
     std::fprintf(stderr, "ERROR: jerasure_matrix_dotprod() called and w is not 1, 8, 16 or 32\n");
     std::exit(1);
   }
-  if (w == 8) {
+  if (w != 1 && whole_words(w, size)) {
     check("jerasure_matrix_dotprod",
           ecgpu_jerasure_matrix_dotprod(k, w, matrix_row, src_ids, dest_id, data_ptrs, coding_ptrs, size));
     return;

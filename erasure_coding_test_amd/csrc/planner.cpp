@@ -45,9 +45,14 @@ void LinearTracker::xor3(void* r1, void* r2, void* r3) {
 
 void LinearTracker::mul(void* src, int c, void* dst, bool add) {
   const int s = id(src), d = id(dst);
-  const auto& T = gf8().mul[c & 0xFF];
   Vec v = state(s);
-  for (auto& x : v) x = T[x];
+  if (w_ == 8) {
+    const auto& T = gf8().mul[c & 0xFF];
+    for (auto& x : v) x = T[x];
+  } else {
+    const uint32_t cw = w_ == 32 ? uint32_t(c) : uint32_t(c) & ((1u << w_) - 1u);
+    for (auto& x : v) x = x ? gf_mul_poly(x, cw, w_) : 0u;
+  }
   if (add) {
     const Vec& old = state(d);
     for (size_t i = 0; i < v.size(); ++i) v[i] ^= old[i];
@@ -115,6 +120,7 @@ FusedOp LinearTracker::finish() const {
     op.dsts.push_back(bufs_[outs[r]]);
     if (col[outs[r]] >= 0) op.dst_is_src = true;
   }
+  op.w = w_;
   op.xor_bytes = xor_;
   op.gf_bytes = gf_;
   op.memcpy_bytes = memcpy_;
@@ -141,7 +147,7 @@ int plan_decode(LinearTracker& t, int k, int m, const int* matrix, int row_k_one
   if (edd > 1 || (edd > 0 && (!row_k_ones || erased[k]))) {
     dm.resize(size_t(k) * k);
     dm_ids.resize(size_t(k));
-    if (make_decoding_matrix(k, m, 8, matrix, erased, dm.data(), dm_ids.data()) < 0) {
+    if (make_decoding_matrix(k, m, t.w(), matrix, erased, dm.data(), dm_ids.data()) < 0) {
       std::free(erased);
       return -1;
     }

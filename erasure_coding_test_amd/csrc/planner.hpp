@@ -2,7 +2,8 @@
 //
 // The reference computes encode/decode as a SEQUENCE of whole-region ops
 // (memcpy, XOR, multiply-add) over caller buffers (jerasure.cpp:561-620,
-// :153-254).  Every op is GF(2^8)-linear, so the final content of each
+// :153-254).  Every op is GF(2^w)-linear (w = 8, 16 or 32; the word size only
+// changes the field the coefficients live in), so the final content of each
 // written buffer is a fixed linear combination of the ORIGINAL contents of
 // the buffers involved.  The tracker replays the sequence on coefficient
 // vectors (one per buffer, indexed by buffer identity = pointer) and emits a
@@ -20,7 +21,8 @@ namespace ecgpu {
 struct FusedOp {
   std::vector<void*> srcs;     // buffers whose ORIGINAL contents are read
   std::vector<void*> dsts;     // buffers written (final contents)
-  std::vector<uint8_t> coef;   // dsts.size() x srcs.size(), row-major
+  std::vector<uint32_t> coef;  // dsts.size() x srcs.size(), row-major, GF(2^w) elements
+  int w = 8;                   // field / word size of the coefficients
   // Reference byte counters (jerasure.cpp:42-44): xor, gf-multiply, memcpy.
   double xor_bytes = 0, gf_bytes = 0, memcpy_bytes = 0;
   bool dst_is_src = false;     // some output buffer is also read
@@ -28,15 +30,18 @@ struct FusedOp {
 
 class LinearTracker {
  public:
+  explicit LinearTracker(int w = 8) : w_(w) {}
+  int w() const { return w_; }
+
   // Registers (or finds) a buffer; identity is the pointer value.
   int id(void* p);
 
-  // Whole-region primitives (GF(2^8)).
+  // Whole-region primitives over GF(2^w).
   void copy(void* dst, void* src);                 // dst = src
   void xor3(void* r1, void* r2, void* r3);         // r3 = r1 ^ r2
   void mul(void* src, int c, void* dst, bool add);  // dst (^)= c * src
 
-  // jerasure_matrix_dotprod semantics (jerasure.cpp:561-620), w = 8, with
+  // jerasure_matrix_dotprod semantics (jerasure.cpp:561-620), any w, with
   // its stats accounting.  size only feeds the byte counters.
   void dotprod(int k, const int* row, const int* src_ids, int dest_id, char** data, char** coding, int64_t size);
 
@@ -50,7 +55,8 @@ class LinearTracker {
   FusedOp finish() const;
 
  private:
-  using Vec = std::vector<uint8_t>;
+  using Vec = std::vector<uint32_t>;
+  int w_ = 8;
   Vec& state(int b);
   std::vector<void*> bufs_;
   std::unordered_map<void*, int> idx_;
@@ -59,10 +65,10 @@ class LinearTracker {
   double xor_ = 0, gf_ = 0, memcpy_ = 0;
 };
 
-// jerasure_matrix_encode (jerasure.cpp:285-299) as a fused op, w = 8.
+// jerasure_matrix_encode (jerasure.cpp:285-299) as a fused op, w = t.w().
 void plan_encode(LinearTracker& t, int k, int m, const int* matrix, char** data, char** coding, int64_t size);
 
-// jerasure_matrix_decode (jerasure.cpp:153-254) as a fused op, w = 8.
+// jerasure_matrix_decode (jerasure.cpp:153-254) as a fused op, w = t.w().
 // Returns 0, or -1 where the reference returns -1 (too many erasures,
 // singular survivor matrix); nothing is recorded in that case.
 int plan_decode(LinearTracker& t, int k, int m, const int* matrix, int row_k_ones, const int* erasures, char** data,

@@ -5,8 +5,9 @@ Same names, argument order and meaning as the reference:
 tensors are used in place; CPU tensors or numpy arrays are staged through
 HBM), ``matrix`` is the flat row-major m x k coding matrix, ``erasures`` the
 erased ids (a trailing -1 is optional).  Encode/decode/dotprod run on the
-MI355X and are synchronous; a HIP failure raises ``EcgpuError`` (there is no
-CPU fallback).  Where the reference calls exit(1) (bad w) this raises
+MI355X for w = 8, 16 and 32 (w = 16 / 32: size a whole number of words) and
+are synchronous; a HIP failure raises ``EcgpuError`` (there is no CPU
+fallback).  Where the reference calls exit(1) (bad w) this raises
 ValueError; where it returns -1 this returns -1.
 """
 from __future__ import annotations
@@ -25,8 +26,8 @@ def _erasure_list(erasures: Sequence[int]) -> list:
 
 
 def jerasure_matrix_encode(k: int, m: int, w: int, matrix, data_ptrs, coding_ptrs, size: int) -> None:
-    if w != 8:
-        raise ValueError("jerasure_matrix_encode: the MI355X path implements w = 8")
+    if w not in (8, 16, 32):
+        raise ValueError("jerasure_matrix_encode: w must be 8, 16 or 32")
     rc = N.lib.ecgpu_jerasure_matrix_encode(k, m, w, N.int_array(matrix), N.ptr_array(addrs(data_ptrs)),
                                             N.ptr_array(addrs(coding_ptrs)), size)
     N.check(rc, "jerasure_matrix_encode")
@@ -34,8 +35,8 @@ def jerasure_matrix_encode(k: int, m: int, w: int, matrix, data_ptrs, coding_ptr
 
 def jerasure_matrix_decode(k: int, m: int, w: int, matrix, row_k_ones: int, erasures, data_ptrs, coding_ptrs,
                            size: int) -> int:
-    if w != 8:
-        raise ValueError("jerasure_matrix_decode: the MI355X path implements w = 8")
+    if w not in (8, 16, 32):
+        return -1  # jerasure.cpp:165
     rc = N.lib.ecgpu_jerasure_matrix_decode(k, m, w, N.int_array(matrix), row_k_ones,
                                             N.int_array(_erasure_list(erasures)), N.ptr_array(addrs(data_ptrs)),
                                             N.ptr_array(addrs(coding_ptrs)), size)
@@ -44,8 +45,8 @@ def jerasure_matrix_decode(k: int, m: int, w: int, matrix, row_k_ones: int, eras
 
 def jerasure_matrix_dotprod(k: int, w: int, matrix_row, src_ids: Optional[Sequence[int]], dest_id: int, data_ptrs,
                             coding_ptrs, size: int) -> None:
-    if w != 8:
-        raise ValueError("jerasure_matrix_dotprod: the MI355X path implements w = 8")
+    if w not in (8, 16, 32):
+        raise ValueError("jerasure_matrix_dotprod: w must be 8, 16 or 32")
     ids = None if src_ids is None else N.int_array(src_ids)
     rc = N.lib.ecgpu_jerasure_matrix_dotprod(k, w, N.int_array(matrix_row), ids, dest_id,
                                              N.ptr_array(addrs(data_ptrs)), N.ptr_array(addrs(coding_ptrs)), size)

@@ -6,6 +6,11 @@ three HIP streams (ecgpu_pipeline_* in include/ecgpu.h).  ``submit`` returns
 a ticket immediately; the buffers must stay untouched until ``wait(ticket)``.
 Pinned buffers (torch ``pin_memory()`` or :func:`host_register`) get
 asynchronous DMA; pageable ones are staged by HIP.
+
+``HostPipeline.decoder`` is the read path (client_main.cpp:2055-2182, decode
+after recv): the fused map of jerasure_matrix_decode for one erasure pattern;
+``submit`` takes the full data[k] / coding[m] buffer lists like the reference
+decode and writes the erased shards back in place.
 """
 from __future__ import annotations
 
@@ -16,16 +21,34 @@ from ._buffers import addr, addrs
 
 
 class HostPipeline:
-    def __init__(self, k: int, m: int, matrix: Sequence[int], size: int, depth: int = 3, device: int = -1):
+    def __init__(self, k: int, m: int, matrix: Sequence[int], size: int, depth: int = 3, device: int = -1,
+                 _handle=None):
         self.k, self.m, self.size = k, m, size
-        self._p = N.lib.ecgpu_pipeline_create(k, m, N.int_array(matrix), size, depth, device)
+        self._p = _handle if _handle is not None else N.lib.ecgpu_pipeline_create(
+            k, m, N.int_array(matrix), size, depth, device)
         if not self._p:
             raise N.EcgpuError(f"ecgpu_pipeline_create failed: {N.last_error()}")
         self._keep = {}  # ticket -> buffers (kept alive until waited)
 
+    @classmethod
+    def decoder(cls, k: int, m: int, matrix: Sequence[int], erasures: Sequence[int], size: int,
+                row_k_ones: int = 0, depth: int = 3, device: int = -1) -> "HostPipeline":
+        """Raises EcgpuError where the reference decode would return -1."""
+        er = list(erasures)
+        if not er or er[-1] != -1:
+            er.append(-1)
+        h = N.lib.ecgpu_pipeline_create_decode(k, m, 8, N.int_array(matrix), row_k_ones, N.int_array(er), size,
+                                               depth, device)
+        if not h:
+            raise N.EcgpuError(f"ecgpu_pipeline_create_decode failed: {N.last_error()}")
+        return cls(k, m, matrix, size, depth, device, _handle=h)
+
     def submit(self, data_ptrs, coding_ptrs) -> int:
         if len(data_ptrs) != self.k or len(coding_ptrs) != self.m:
             raise ValueError("k data and m coding buffers required")
+        for b in list(data_ptrs) + list(coding_ptrs):
+            if getattr(b, "is_cuda", False):
+                raise ValueError("HostPipeline takes host buffers; use encode_plan/DecodePlan for HBM shards")
         t = N.lib.ecgpu_pipeline_submit(self._p, N.ptr_array(addrs(data_ptrs)), N.ptr_array(addrs(coding_ptrs)))
         if t < 0:
             raise N.EcgpuError(f"ecgpu_pipeline_submit failed ({t}): {N.last_error()}")

@@ -28,7 +28,7 @@ def reed_sol_r6_coding_matrix(k: int, w: int) -> Optional[List[int]]:
 
 
 def reed_sol_r6_encode(k: int, w: int, data_ptrs, coding_ptrs, size: int) -> int:
-    """RAID-6 P/Q encode (reed_sol.cpp:200-225); w must be 8 here."""
+    """RAID-6 P/Q encode (reed_sol.cpp:200-225): 1, or 0 for w not in {8, 16, 32}."""
     return N.check(N.lib.ecgpu_reed_sol_r6_encode(k, w, N.ptr_array(addrs(data_ptrs)),
                                                   N.ptr_array(addrs(coding_ptrs)), size), "reed_sol_r6_encode")
 
@@ -37,3 +37,15 @@ def reed_sol_galois_w08_region_multby_2(region, nbytes: int) -> None:
     from ._buffers import addr
     N.check(N.lib.ecgpu_reed_sol_galois_w08_region_multby_2(addr(region), nbytes),
             "reed_sol_galois_w08_region_multby_2")
+
+
+def reed_sol_galois_w16_region_multby_2(region, nbytes: int) -> None:
+    from ._buffers import addr
+    N.check(N.lib.ecgpu_reed_sol_galois_w16_region_multby_2(addr(region), nbytes),
+            "reed_sol_galois_w16_region_multby_2")
+
+
+def reed_sol_galois_w32_region_multby_2(region, nbytes: int) -> None:
+    from ._buffers import addr
+    N.check(N.lib.ecgpu_reed_sol_galois_w32_region_multby_2(addr(region), nbytes),
+            "reed_sol_galois_w32_region_multby_2")

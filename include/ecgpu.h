@@ -13,8 +13,10 @@
  *
  * Hot path (GPU): ecgpu_jerasure_matrix_encode / _decode / _dotprod,
  * ecgpu_galois_w08_region_multiply, ecgpu_galois_region_xor,
- * ecgpu_jerasure_do_parity, ecgpu_reed_sol_r6_encode (w=8) and the batched
- * device-resident plan API below.  These accept host OR device pointers
+ * ecgpu_jerasure_do_parity, ecgpu_reed_sol_r6_encode and the batched
+ * device-resident plan API below.  The matrix calls take w = 8 (the north
+ * star), 16 or 32 (wide-word kernels; size a whole number of w/8-byte words,
+ * else ECGPU_ERR_ARG) and so do the w16/w32 region functions.  These accept host OR device pointers
  * (classified per buffer; host buffers are staged through HBM) and are
  * synchronous: results are valid on return, like the reference.  They never
  * fall back to a CPU path; a HIP failure returns ECGPU_ERR_HIP (or, through
@@ -78,12 +80,12 @@ ECGPU_API int ecgpu_jerasure_make_decoding_matrix(int k, int m, int w, int* matr
  * 0..k+m-1.  On return out_ids[0..*n_out) are the shard ids written,
  * src_ids[0..*n_src) the shard ids read, coefs row-major n_out x n_src.
  * Arrays must hold k+m (ids) and (k+m)^2 (coefs) entries.  Returns 0 or -1
- * exactly where the reference decode returns -1.  w must be 8. */
+ * exactly where the reference decode returns -1.  w = 8, 16 or 32. */
 ECGPU_API int ecgpu_decode_plan(int k, int m, int w, const int* matrix, int row_k_ones, const int* erasures,
                                 int* out_ids, int* n_out, int* src_ids, int* n_src, int* coefs);
 
 /* ------------------------------------ hot path: reference semantics ----- */
-/* jerasure.cpp:285-299.  w must be 8 (w=16/32 live in the drop-in library). */
+/* jerasure.cpp:285-299.  w = 8, 16 or 32. */
 ECGPU_API int ecgpu_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs,
                                            int size);
 /* jerasure.cpp:153-254.  Returns 0 / -1 like the reference. */
@@ -98,9 +100,15 @@ ECGPU_API int ecgpu_jerasure_do_parity(int k, char** data_ptrs, char* parity_ptr
 ECGPU_API int ecgpu_galois_w08_region_multiply(char* region, int multby, int nbytes, char* r2, int add);
 /* galois.cpp:731-754 */
 ECGPU_API int ecgpu_galois_region_xor(char* r1, char* r2, char* r3, int nbytes);
-/* reed_sol.cpp:200-225 (w = 8) and reed_sol.cpp:112-152 */
+/* galois.cpp:469-542 (nbytes/2 words) and galois.cpp:666-727 (nbytes/4 words) */
+ECGPU_API int ecgpu_galois_w16_region_multiply(char* region, int multby, int nbytes, char* r2, int add);
+ECGPU_API int ecgpu_galois_w32_region_multiply(char* region, int multby, int nbytes, char* r2, int add);
+/* reed_sol.cpp:200-225 (returns 1; 0 for w other than 8/16/32) and the
+ * multiply-by-2 helpers reed_sol.cpp:112-152, :158-198, :90-106 */
 ECGPU_API int ecgpu_reed_sol_r6_encode(int k, int w, char** data_ptrs, char** coding_ptrs, int size);
 ECGPU_API int ecgpu_reed_sol_galois_w08_region_multby_2(char* region, int nbytes);
+ECGPU_API int ecgpu_reed_sol_galois_w16_region_multby_2(char* region, int nbytes);
+ECGPU_API int ecgpu_reed_sol_galois_w32_region_multby_2(char* region, int nbytes);
 /* jerasure.cpp:1143-1151: fills xor, gf, memcpy byte counts and resets. */
 ECGPU_API int ecgpu_jerasure_get_stats(double* fill_in);
 
@@ -145,6 +153,14 @@ ECGPU_API void ecgpu_accum_destroy(ecgpu_accum* a);
 typedef struct ecgpu_pipeline ecgpu_pipeline;
 ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create(int k, int m, const int* matrix, int64_t size, int depth,
                                                 int device);
+/* Read path (client_main.cpp:2055-2182, decode after recv): the same ring
+ * running the fused map of jerasure_matrix_decode (jerasure.cpp:153-254) for
+ * one erasure pattern.  submit takes the caller's full data_ptrs[k] /
+ * coding_ptrs[m] like the reference decode: the survivors it reads are copied
+ * in, the erased shards are written back in place.  NULL (ecgpu_last_error)
+ * where the reference decode returns -1. */
+ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create_decode(int k, int m, int w, const int* matrix, int row_k_ones,
+                                                       const int* erasures, int64_t size, int depth, int device);
 ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, char** coding_ptrs); /* <0: error */
 ECGPU_API int ecgpu_pipeline_wait(ecgpu_pipeline* p, int64_t ticket);
 ECGPU_API int ecgpu_pipeline_drain(ecgpu_pipeline* p);

@@ -494,3 +494,129 @@ def test_host_pipeline_matches_oracle(ec, gpu, restatement, memory):
         for bufs in data + coding:
             for b in bufs:
                 ec.pipeline.host_unregister(b)
+
+
+@pytest.mark.parametrize("erasures", [[0], [0, 1, 2, 3], [2, 11], [10, 13], []])
+def test_host_pipeline_decoder_matches_reference_decode(ec, gpu, erasures):
+    import torch
+    k, m, size, stripes = 10, 4, (1 << 20) + 5, 5
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    full = []
+    for s in range(stripes):
+        data = host_shards(41, s, k, size)
+        coding = alloc_shards(m, size, PAD)
+        ec.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, size)
+        full.append(data + coding)
+    want = [[b.copy() for b in st] for st in full]
+    # pinned copies with the erased shards scribbled over
+    bufs = [[torch.from_numpy(b).pin_memory() for b in st] for st in full]
+    for st in bufs:
+        for e in erasures:
+            st[e].fill_(0xA5)
+    p = ec.HostPipeline.decoder(k, m, M, erasures, size, depth=2)
+    for st in bufs:
+        p.submit(st[:k], st[k:])
+    p.drain()
+    p.close()
+    for s in range(stripes):
+        for i in range(k + m):
+            assert np.array_equal(bufs[s][i].numpy()[:size], want[s][i][:size]), (s, i)
+
+
+def test_host_pipeline_decoder_rejects_undecodable(ec, gpu):
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(6, 3, 8)
+    with pytest.raises(ec._native.EcgpuError):
+        ec.HostPipeline.decoder(6, 3, M, [0, 1, 2, 3], 4096)
+
+
+# ------------------------------------------- wide words (w = 16 / 32) ----
+def _ref_nsa():
+    import ctypes
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                        "libjerasure_ref_nsa.so")
+    if not os.path.exists(path):
+        pytest.skip("oracle/_ref/libjerasure_ref_nsa.so not built")
+    L = ctypes.CDLL(path)
+    I, IP, PP = ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p)
+    L._Z22jerasure_matrix_encodeiiiPiPPcS1_i.argtypes = [I, I, I, IP, PP, PP, I]
+    L._Z22jerasure_matrix_decodeiiiPiiS_PPcS1_i.argtypes = [I, I, I, IP, I, IP, PP, PP, I]
+    return L
+
+
+def _cints(v):
+    import ctypes
+    return (ctypes.c_int * len(v))(*v)
+
+
+def _cptrs(bufs):
+    import ctypes
+    return (ctypes.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+
+
+@pytest.mark.parametrize("w", [16, 32])
+@pytest.mark.parametrize("size,offset", [(1 << 20, 0), ((1 << 20) + 8, 0), (65536 + 4, 4), (4, 0)])
+def test_wide_word_matrix_coding_device(ec, gpu, w, size, offset):
+    """w = 16 / 32 encode + decode on device tensors (16-B column kernel,
+    word-tail kernel, misaligned base) against the reference library."""
+    import torch
+    if size % (w // 8):
+        pytest.skip("not whole words")
+    ref = _ref_nsa()
+    k, m = 6, 3
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w)
+    rng = np.random.default_rng(w * 7 + size)
+    data = [rng.integers(0, 256, size + 64, dtype=np.uint8) for _ in range(k)]
+    coding = [np.zeros(size + 64, np.uint8) for _ in range(m)]
+    ref._Z22jerasure_matrix_encodeiiiPiPPcS1_i(k, m, w, _cints(M), _cptrs(data), _cptrs(coding), size)
+
+    def dev(a):
+        t = torch.zeros(size + offset + 16, dtype=torch.uint8, device=gpu)
+        v = t[offset:offset + size]
+        v.copy_(torch.from_numpy(a[:size]))
+        return v
+    dd = [dev(a) for a in data]
+    dc = [torch.full((size + offset + 16,), 0x5A, dtype=torch.uint8, device=gpu)[offset:offset + size]
+          for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, w, M, dd, dc, size)
+    torch.cuda.synchronize()
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
+    # decode two data + one parity erasure
+    er = [1, 4, k + 2]
+    for e in er:
+        (dd + dc)[e].fill_(0)
+    assert ec.jerasure.jerasure_matrix_decode(k, m, w, M, 0, er, dd, dc, size) == 0
+    torch.cuda.synchronize()
+    for j in range(k):
+        assert np.array_equal(dd[j].cpu().numpy(), data[j][:size]), j
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
+
+
+@pytest.mark.parametrize("w", [16, 32])
+def test_wide_word_region_ops_device(ec, gpu, w):
+    import torch
+    size = 8192 + 8
+    rng = np.random.default_rng(w)
+    src = rng.integers(0, 256, size, dtype=np.uint8)
+    dst = rng.integers(0, 256, size, dtype=np.uint8)
+    mulfn = ec.galois.galois_w16_region_multiply if w == 16 else ec.galois.galois_w32_region_multiply
+    W = w // 8
+    c = 0xBEEF if w == 16 else 0x12345678
+    sw = src.view(np.uint16 if w == 16 else np.uint32)
+    dw = dst.view(np.uint16 if w == 16 else np.uint32)
+    prod = np.array([ec.galois.galois_single_multiply(int(x), c, w) & 0xFFFFFFFF for x in sw], dtype=sw.dtype)
+    ts, td = torch.from_numpy(src).to(gpu), torch.from_numpy(dst).to(gpu)
+    mulfn(ts, c, size, td, 1)
+    torch.cuda.synchronize()
+    assert np.array_equal(td.cpu().numpy().view(dw.dtype), dw ^ prod)
+    mulfn(ts, c, size, td, 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(td.cpu().numpy().view(dw.dtype), prod)
+    by2 = ec.reed_sol.reed_sol_galois_w16_region_multby_2 if w == 16 else ec.reed_sol.reed_sol_galois_w32_region_multby_2
+    by2(ts, size)
+    torch.cuda.synchronize()
+    two = np.array([ec.galois.galois_single_multiply(int(x), 2, w) & 0xFFFFFFFF for x in sw], dtype=sw.dtype)
+    assert np.array_equal(ts.cpu().numpy().view(sw.dtype), two)
+    assert W in (2, 4)

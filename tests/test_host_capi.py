@@ -7,6 +7,10 @@ golden inconsistent-input decode cases: matching the reference's digests pins
 the planner's survivor choice, row_k_ones path and aliasing semantics without
 a GPU.
 """
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -137,3 +141,31 @@ def test_recommended_stride():
     from erasure_coding_test_amd import _native as N
     assert N.lib.ecgpu_recommended_shard_stride(4 << 20) == (4 << 20) + 4096
     assert N.lib.ecgpu_recommended_shard_stride(1) % 256 == 0
+
+
+NO_GPU = not os.path.exists("/dev/kfd")
+
+
+@pytest.mark.skipif(not NO_GPU, reason="checks the no-GPU failure mode")
+def test_hot_path_without_gpu_fails_loudly():
+    """No silent success and no CPU fallback: with no GPU every hot-path call
+    returns ECGPU_ERR_HIP with a message, and the drop-in aborts."""
+    from erasure_coding_test_amd import _native as N
+    a = np.arange(64, dtype=np.uint8)
+    b = np.zeros(64, np.uint8)
+    before = b.copy()
+    for fn, args in (("ecgpu_galois_region_xor", (a.ctypes.data, a.ctypes.data, b.ctypes.data, 64)),
+                     ("ecgpu_galois_w08_region_multiply", (a.ctypes.data, 7, 64, b.ctypes.data, 0)),
+                     ("ecgpu_galois_w16_region_multiply", (a.ctypes.data, 0, 64, b.ctypes.data, 0)),
+                     ("ecgpu_galois_w32_region_multiply", (a.ctypes.data, 9, 64, b.ctypes.data, 1))):
+        assert getattr(N.lib, fn)(*args) == -3, fn
+        assert N.last_error(), fn
+        assert np.array_equal(b, before), fn
+    code = ("import ctypes, numpy as np\n"
+            f"L = ctypes.CDLL({os.path.join(os.path.dirname(N.LIB_PATH), 'libjerasure_amd.so')!r})\n"
+            "f = L._Z17galois_region_xorPcS_S_i\n"
+            "f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int]\n"
+            "a = np.zeros(64, np.uint8)\n"
+            "f(a.ctypes.data, a.ctypes.data, a.ctypes.data, 64)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "MI355X path failed" in r.stderr

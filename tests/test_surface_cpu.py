@@ -2,7 +2,9 @@
 reference library, both driven by their C++-mangled names through ctypes:
 w=16/32 field and region math, w=16/32 matrix coding, RAID-6 for w=16/32,
 bit-matrices, dumb/smart XOR schedules, scheduled encode/decode and the
-schedule cache.  Nothing here touches the GPU.
+schedule cache.  The w=16/32 region calls and whole-word matrix coding run on
+the MI355X (wide-word kernels) and are gpu-marked; the rest never touches
+the GPU.
 """
 import ctypes
 import os
@@ -115,33 +117,48 @@ def test_mult_div_tables(libs):
     assert not mine.get_mult(14) and not ref.get_mult(14)
 
 
+WHOLE = 4096  # whole words: the MI355X wide-word path (gpu-marked cases)
+
+
+def _ragged(w):
+    # a size that is not whole w/8-byte words: the drop-in's exact-word CPU
+    # restatement (the reference itself reads/writes past the region here,
+    # so only the whole-word prefix is compared)
+    return 4095 if w == 16 else 4094
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size", [WHOLE, 4094, 4095])
 @pytest.mark.parametrize("w", [16, 32])
-def test_region_math_w16_w32(libs, w):
+def test_region_math_w16_w32(libs, w, size):
+    """galois_w16/w32_region_multiply and the multby_2 helpers run on the
+    MI355X for every size (whole words; a ragged tail is not touched)."""
     ref, mine = libs
-    rng = np.random.default_rng(w)
+    rng = np.random.default_rng(w + size)
     f = "w16" if w == 16 else "w32"
+    n = size - size % (w // 8)
     for multby in (0, 1, 2, 0x1234, 0xBEEF) + ((0x12345678,) if w == 32 else ()):
         for add in (0, 1):
             for inplace in (False, True):
-                size = 4096
                 src = rand_bufs(rng, 1, size)[0]
                 dst = rand_bufs(rng, 1, size)[0]
                 s1, d1, s2, d2 = src.copy(), dst.copy(), src.copy(), dst.copy()
                 getattr(ref, f)(s1.ctypes.data, multby, size, None if inplace else d1.ctypes.data, add)
                 getattr(mine, f)(s2.ctypes.data, multby, size, None if inplace else d2.ctypes.data, add)
-                assert np.array_equal(s1[:size], s2[:size]) and np.array_equal(d1[:size], d2[:size]), (multby, add)
-    buf = rand_bufs(rng, 1, 4096)[0]
+                assert np.array_equal(s1[:n], s2[:n]) and np.array_equal(d1[:n], d2[:n]), (multby, add, inplace)
+                assert np.array_equal(s2[n:], src[n:]) and np.array_equal(d2[n:], dst[n:])
+    buf = rand_bufs(rng, 1, size)[0]
     b1, b2 = buf.copy(), buf.copy()
-    getattr(ref, "by2_16" if w == 16 else "by2_32")(b1.ctypes.data, 4096)
-    getattr(mine, "by2_16" if w == 16 else "by2_32")(b2.ctypes.data, 4096)
-    assert np.array_equal(b1[:4096], b2[:4096])
+    n4 = size - size % 4  # the reference helpers step in 4-byte ints
+    getattr(ref, "by2_16" if w == 16 else "by2_32")(b1.ctypes.data, size)
+    getattr(mine, "by2_16" if w == 16 else "by2_32")(b2.ctypes.data, size)
+    assert np.array_equal(b1[:n4], b2[:n4])
 
 
-@pytest.mark.parametrize("w", [16, 32])
-def test_matrix_coding_w16_w32(libs, w):
+def _matrix_coding(libs, w, size, cmp):
     ref, mine = libs
     rng = np.random.default_rng(100 + w)
-    k, m, size = 5, 3, 4096
+    k, m = 5, 3
     M = list(np.ctypeslib.as_array(ctypes.cast(ref.vdm(k, m, w), IP), shape=(k * m,)))
     assert M == list(np.ctypeslib.as_array(ctypes.cast(mine.vdm(k, m, w), IP), shape=(k * m,)))
     data = rand_bufs(rng, k, size)
@@ -156,15 +173,29 @@ def test_matrix_coding_w16_w32(libs, w):
             for i in (e, (e + 2) % (k + m)):
                 (d2 + c2)[i][:size] = 0
             assert L.decode(k, m, w, ints(M), 0, ints([e, (e + 2) % (k + m), -1]), ptrs(d2), ptrs(c2), size) == 0
-            outs.append([x[:size].copy() for x in d2 + c2])
-        outs.append([x[:size].copy() for x in c])
+            outs.append([x[:cmp].copy() for x in d2 + c2])
+        outs.append([x[:cmp].copy() for x in c])
         r6c = [np.zeros(size + 64, np.uint8) for _ in range(2)]
         assert L.r6_encode(k, w, ptrs(d), ptrs(r6c), size) == 1
-        outs.append([x[:size].copy() for x in r6c])
+        outs.append([x[:cmp].copy() for x in r6c])
     half = len(outs) // 2
     for a, b in zip(outs[:half], outs[half:]):
         for x, y in zip(a, b):
             assert np.array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w", [16, 32])
+def test_matrix_coding_w16_w32_gpu(libs, w):
+    """Whole-word sizes: encode / decode / RAID-6 on the wide-word kernels."""
+    _matrix_coding(libs, w, WHOLE, WHOLE)
+
+
+@pytest.mark.parametrize("w", [16, 32])
+def test_matrix_coding_w16_w32_ragged_cpu(libs, w):
+    """Ragged sizes: the CPU restatement, compared on the whole-word prefix."""
+    size = _ragged(w)
+    _matrix_coding(libs, w, size, size - size % (w // 8))
 
 
 def read_schedule(addr):

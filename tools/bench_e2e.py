@@ -10,6 +10,8 @@ originate and terminate in host memory sees, and the other BASELINE configs.
   e2e_pipeline same stripes through the C-level HostPipeline
                (ecgpu_pipeline_*): per-shard H2D/D2H on its own streams,
                pinned and pageable source buffers.
+  e2e_read_pipeline  the read path: ecgpu_pipeline_create_decode over the
+               same pinned stripes (10 survivors in, erased shards out).
   dropin_pageable  jerasure_matrix_encode / _decode straight on malloc'd
                (pageable) numpy buffers through the C ABI -- the reference
                client's call shape (client_main.cpp:1060, :2118).
@@ -138,6 +140,35 @@ def e2e_pipeline(stripes=48, k=10, m=4, S=4 << 20, depth=3, pinned=True):
             "data_GiBps": round(stripes * k * S / t / GiB, 2), "parity_ok": ok}
 
 
+def e2e_read_pipeline(erasures, stripes=48, k=10, m=4, S=4 << 20, depth=3):
+    """Read path: survivors pinned host -> HBM -> decode -> erased shards back."""
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    host = torch.empty((stripes, k + m, S), dtype=torch.uint8).pin_memory()
+    host[:, :k].random_(0, 256)
+    enc = E.HostPipeline(k, m, M, S, depth=depth)
+    for s in range(stripes):
+        enc.submit([host[s, j] for j in range(k)], [host[s, k + i] for i in range(m)])
+    enc.drain()
+    enc.close()
+    want = host[stripes - 1].clone()
+    p = E.HostPipeline.decoder(k, m, M, erasures, S, depth=depth)
+
+    def run():
+        for s in range(stripes):
+            p.submit([host[s, j] for j in range(k)], [host[s, k + i] for i in range(m)])
+        p.drain()
+
+    run()
+    host[stripes - 1, erasures] = 0
+    t0 = time.perf_counter()
+    run()
+    t = time.perf_counter() - t0
+    p.close()
+    return {"workload": f"RS(10,4) 4 MiB decode {erasures} via ecgpu_pipeline_create_decode, {stripes} stripes "
+                        f"pinned host, depth {depth}",
+            "data_GiBps": round(stripes * k * S / t / GiB, 2), "parity_ok": bool(torch.equal(host[stripes - 1], want))}
+
+
 def dropin_pageable(k=10, m=4, S=4 << 20, reps=5):
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     rng = np.random.default_rng(0)
@@ -197,6 +228,8 @@ def main():
     a = ap.parse_args()
     res = {"pcie": pcie_rates(), "e2e_pinned": e2e_pinned(a.stripes),
            "e2e_pipeline_pinned": e2e_pipeline(a.stripes), "e2e_pipeline_pageable": e2e_pipeline(a.stripes, pinned=False),
+           "e2e_read_pipeline_1": e2e_read_pipeline([0], a.stripes),
+           "e2e_read_pipeline_4": e2e_read_pipeline([0, 1, 2, 3], a.stripes),
            "dropin_pageable": dropin_pageable(),
            "device_configs": device_configs()}
     print(json.dumps(res, indent=1))

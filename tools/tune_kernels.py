@@ -55,7 +55,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--stripes", type=int, default=24)
     ap.add_argument("--pads", default="0", help="comma list of per-shard padding bytes (shard stride = S + pad)")
-    ap.add_argument("--only", default="", help="substring filter on variant names")
+    ap.add_argument("--only", default="", help="comma list of substrings; keep variants matching any")
     args = ap.parse_args()
     k, m, S, B = 10, 4, 4 << 20, args.stripes
     results = []
@@ -130,7 +130,8 @@ def run_layout(args, k, m, S, B, pad):
         ud, zd = masks(dec_rows["ones"])
         variants.append((f"V dec1 vec{vec}", 8, 10, 1, vec, 4, qd, nd, src_dec, dst_dec, B, ud, zd,
                          (k + 1) * S * B, 1))
-    variants = [v for v in variants if args.only in v[0]]
+    only = [o for o in args.only.split(",")] if args.only else [""]
+    variants = [v for v in variants if any(o in v[0] for o in only)]
     times = {v[0]: [] for v in variants}
     import random
     order = list(variants)

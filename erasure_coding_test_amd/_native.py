@@ -53,6 +53,10 @@ SIGNATURES = {
     "ecgpu_jerasure_matrix_multiply": (c_void_p, [c_int_p, c_int_p, c_int, c_int, c_int, c_int, c_int]),
     "ecgpu_jerasure_erasures_to_erased": (c_void_p, [c_int, c_int, c_int_p]),
     "ecgpu_jerasure_make_decoding_matrix": (c_int, [c_int, c_int, c_int, c_int_p, c_int_p, c_int_p, c_int_p]),
+    "ecgpu_jerasure_matrix_to_bitmatrix": (c_void_p, [c_int, c_int, c_int, c_int_p]),
+    "ecgpu_jerasure_make_decoding_bitmatrix": (c_int, [c_int, c_int, c_int, c_int_p, c_int_p, c_int_p, c_int_p]),
+    "ecgpu_jerasure_invert_bitmatrix": (c_int, [c_int_p, c_int_p, c_int]),
+    "ecgpu_jerasure_invertible_bitmatrix": (c_int, [c_int_p, c_int]),
     "ecgpu_decode_plan": (c_int, [c_int, c_int, c_int, c_int_p, c_int, c_int_p, c_int_p, c_int_p, c_int_p,
                                   c_int_p, c_int_p]),
     "ecgpu_jerasure_matrix_encode": (c_int, [c_int, c_int, c_int, c_int_p, c_void_pp, c_void_pp, c_int]),
@@ -64,6 +68,12 @@ SIGNATURES = {
     "ecgpu_galois_region_xor": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     "ecgpu_reed_sol_r6_encode": (c_int, [c_int, c_int, c_void_pp, c_void_pp, c_int]),
     "ecgpu_reed_sol_galois_w08_region_multby_2": (c_int, [c_void_p, c_int]),
+    "ecgpu_jerasure_bitmatrix_dotprod": (c_int, [c_int, c_int, c_int_p, c_int_p, c_int, c_void_pp, c_void_pp, c_int, c_int]),
+    "ecgpu_jerasure_bitmatrix_encode": (c_int, [c_int, c_int, c_int, c_int_p, c_void_pp, c_void_pp, c_int, c_int]),
+    "ecgpu_jerasure_bitmatrix_decode": (c_int, [c_int, c_int, c_int, c_int_p, c_int, c_int_p, c_void_pp, c_void_pp, c_int, c_int]),
+    "ecgpu_jerasure_do_scheduled_operations": (c_int, [c_void_pp, c_void_p, c_int]),
+    "ecgpu_jerasure_schedule_encode": (c_int, [c_int, c_int, c_int, c_void_p, c_void_pp, c_void_pp, c_int, c_int]),
+    "ecgpu_schedule_run": (c_int, [c_int, c_void_pp, c_void_p, c_int, c_int, c_int]),
     "ecgpu_reed_sol_galois_w16_region_multby_2": (c_int, [c_void_p, c_int]),
     "ecgpu_reed_sol_galois_w32_region_multby_2": (c_int, [c_void_p, c_int]),
     "ecgpu_galois_w16_region_multiply": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int]),

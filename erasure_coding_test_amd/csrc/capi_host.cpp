@@ -57,6 +57,16 @@ ECGPU_API int ecgpu_jerasure_make_decoding_matrix(int k, int m, int w, int* matr
   return make_decoding_matrix(k, m, w, matrix, erased, dm, dm_ids);
 }
 
+ECGPU_API int* ecgpu_jerasure_matrix_to_bitmatrix(int k, int m, int w, int* matrix) {
+  return matrix_to_bitmatrix(k, m, w, matrix);
+}
+ECGPU_API int ecgpu_jerasure_make_decoding_bitmatrix(int k, int m, int w, int* matrix, int* erased, int* dm,
+                                                     int* dm_ids) {
+  return make_decoding_bitmatrix(k, m, w, matrix, erased, dm, dm_ids);
+}
+ECGPU_API int ecgpu_jerasure_invert_bitmatrix(int* mat, int* inv, int rows) { return invert_bitmatrix(mat, inv, rows); }
+ECGPU_API int ecgpu_jerasure_invertible_bitmatrix(int* mat, int rows) { return invertible_bitmatrix(mat, rows); }
+
 // Replays the decode on symbolic buffers whose "pointers" are shard ids + 1,
 // then reads the fused map back in terms of ids.
 ECGPU_API int ecgpu_decode_plan(int k, int m, int w, const int* matrix, int row_k_ones, const int* erasures,

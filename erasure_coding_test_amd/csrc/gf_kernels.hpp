@@ -680,5 +680,97 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_words(ApplyArgs a) {
   }
 }
 
+// ------------------------------------------- GF(2) packet coding ----
+// Bit-matrix and XOR-schedule coding (jerasure.cpp:301-345, :1153-1192): a
+// device is w packets of `packetsize` bytes per super-packet, and every
+// output packet row is the XOR of a set of source packet rows (the host
+// replays the reference's memcpy / XOR sequence symbolically, so aliasing
+// and schedules that reuse earlier outputs fold into one map).  A "packet
+// view" is base + sp * stride + [0, packetsize) for super-packet sp.  Lane g
+// handles 8 bytes of one packet column; output rows <= RT per launch, the
+// row set of source j is the wave-uniform bit mask mask[j], applied as
+// acc ^= x & sext(bit) (one SALU bit extract + one v_bitop3 per term).
+struct PacketArgs {
+  const uint8_t* const* src;  // [nsrc] packet-view bases
+  uint8_t* const* dst;        // [R] packet-view bases
+  const uint32_t* mask;       // [nsrc] bit r: source feeds output row r
+  int64_t sstride, dstride;   // bytes between super-packets (sources / outputs)
+  int64_t cpp;                // 8-byte columns per packet (words kernel) or bytes per packet (bytes kernel)
+  int64_t ncols;              // super-packets * cpp
+  int nsrc, R;
+};
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u32x2 gu32x2;
+
+__device__ __forceinline__ void packet_coords(const PacketArgs& a, int64_t g, int64_t* sp, int64_t* col) {
+  if (a.ncols <= 0xFFFFFFFFll) {  // 32-bit division unless the launch is huge
+    const uint32_t q = uint32_t(g) / uint32_t(a.cpp);
+    *sp = q;
+    *col = int64_t(uint32_t(g) - q * uint32_t(a.cpp));
+  } else {
+    *sp = g / a.cpp;
+    *col = g - *sp * a.cpp;
+  }
+}
+
+template <int RT>
+__device__ __forceinline__ void xor_masked(uint32_t (&acc)[RT][2], const u32x2& x, uint32_t m) {
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const uint32_t sel = uint32_t(int32_t(m << (31 - r)) >> 31);  // 0 or ~0, wave-uniform (SALU)
+    acc[r][0] = __builtin_amdgcn_bitop3_b32(acc[r][0], x.x, sel, 0x78);  // a ^ (b & c): 0xF0 ^ (0xCC & 0xAA)
+    acc[r][1] = __builtin_amdgcn_bitop3_b32(acc[r][1], x.y, sel, 0x78);
+  }
+}
+
+template <int RT>
+__global__ __launch_bounds__(kBlock) void gf_xor_packets(PacketArgs a) {
+  const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= a.ncols) return;
+  int64_t sp, col;
+  packet_coords(a, g, &sp, &col);
+  const int64_t soff = sp * a.sstride + col * 8, doff = sp * a.dstride + col * 8;
+  uint8_t* dp[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) dp[r] = r < a.R ? a.dst[r] : nullptr;
+  uint32_t acc[RT][2];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) acc[r][0] = acc[r][1] = 0u;
+  int j = 0;
+  for (; j + 4 <= a.nsrc; j += 4) {  // four loads in flight before the first use
+    u32x2 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = *(const gu32x2*)(a.src[j + u] + soff);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xor_masked<RT>(acc, x[u], a.mask[j + u]);
+  }
+  for (; j < a.nsrc; ++j) {
+    const u32x2 x = *(const gu32x2*)(a.src[j] + soff);
+    xor_masked<RT>(acc, x, a.mask[j]);
+  }
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+    if (r < a.R) *(gu32x2*)(dp[r] + doff) = u32x2{acc[r][0], acc[r][1]};
+}
+
+// Byte form for packet sizes / bases that are not 8-byte aligned.
+__global__ __launch_bounds__(kBlock) void gf_xor_packets_bytes(PacketArgs a) {
+  const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= a.ncols) return;
+  int64_t sp, col;
+  packet_coords(a, g, &sp, &col);
+  const int64_t soff = sp * a.sstride + col, doff = sp * a.dstride + col;
+  uint8_t out[32];
+  for (int r = 0; r < 32; ++r) out[r] = 0;
+  for (int j = 0; j < a.nsrc; ++j) {
+    const uint8_t x = a.src[j][soff];
+    const uint32_t m = a.mask[j];
+    for (int r = 0; r < a.R; ++r)
+      if ((m >> r) & 1u) out[r] ^= x;
+  }
+  for (int r = 0; r < a.R; ++r) a.dst[r][doff] = out[r];
+}
+
 }  // namespace dev
 }  // namespace ecgpu

@@ -1,9 +1,12 @@
-// jerasure_surface.cpp -- CPU implementation of the reference surface that
-// lies outside the north-star GF(2^8) path: w = 16 / 32 region math and
-// matrix coding, GF(2) bit-matrix coding and XOR schedules
-// (jerasure.cpp:257-345, :623-1032, :1153-1344), matrix printing.  These
-// keep include/dropin/jerasure.h link- and behaviour-compatible; none of the
-// reference's callers uses them.
+// jerasure_surface.cpp -- the reference surface outside the north-star
+// GF(2^8) path: w = 16 / 32 region math and matrix coding (CPU restatement,
+// used for ragged sizes only -- whole-word sizes run on the MI355X, see
+// jerasure_dropin.cpp), GF(2) bit-matrix coding and XOR schedules
+// (jerasure.cpp:257-345, :623-1032, :1153-1344) and matrix printing.  The
+// bit-matrix / schedule EXECUTION runs on the MI355X (ecgpu_jerasure_bitmatrix_*,
+// ecgpu_schedule_run: one fused GF(2) packet map per call) whenever size is a
+// whole number of super-packets; matrix / schedule CONSTRUCTION is host code
+// here.  None of the reference's callers uses this surface.
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -11,6 +14,7 @@
 #include <mutex>
 #include <vector>
 
+#include "ecgpu.h"
 #include "gf_host.hpp"
 // The reference surface is this library's export list (default visibility);
 // everything else is built -fvisibility=hidden.
@@ -28,6 +32,13 @@ double g_stats[3] = {0, 0, 0};
 
 inline char* dev_ptr(int id, int k, char** data, char** coding) { return id < k ? data[id] : coding[id - k]; }
 }  // namespace
+
+// GPU packet-coding calls: a failure is fatal, never a silent CPU fallback.
+void gpu_check(const char* fn, int rc) {
+  if (rc == ECGPU_OK) return;
+  std::fprintf(stderr, "%s: MI355X path failed (%d): %s\n", fn, rc, ecgpu_last_error());
+  std::abort();
+}
 
 int create_log_tables(int w) { return ecgpu::create_log_tables(w); }
 int create_mult_tables(int w) { return ecgpu::create_mult_tables(w); }
@@ -180,6 +191,20 @@ void jerasure_bitmatrix_dotprod(int k, int w, int* bm_row, int* src_ids, int des
     std::fprintf(stderr, "jerasure_bitmatrix_dotprod - size%%(w*packetsize)) must = 0\n");
     std::exit(1);
   }
+  ecgpu_cpu::gpu_check("jerasure_bitmatrix_dotprod", ecgpu_jerasure_bitmatrix_dotprod(
+                                                         k, w, bm_row, src_ids, dest_id, data, coding, size, packetsize));
+}
+
+namespace {
+// The CPU form of jerasure_bitmatrix_dotprod, kept for bitmatrix_decode with a
+// size that is not whole super-packets (the reference exits there, from here).
+void cpu_bitmatrix_dotprod(int k, int w, int* bm_row, int* src_ids, int dest_id, char** data, char** coding,
+                           int size, int packetsize) {
+  const int chunk = w * packetsize;
+  if (size % chunk != 0) {
+    std::fprintf(stderr, "jerasure_bitmatrix_dotprod - size%%(w*packetsize)) must = 0\n");
+    std::exit(1);
+  }
   char* out = dest_id < k ? data[dest_id] : coding[dest_id - k];
   for (int off = 0; off < size; off += chunk) {
     const int* bit = bm_row;
@@ -205,6 +230,8 @@ void jerasure_bitmatrix_dotprod(int k, int w, int* bm_row, int* src_ids, int des
   }
 }
 
+}  // namespace
+
 void jerasure_bitmatrix_encode(int k, int m, int w, int* bitmatrix, char** data, char** coding, int size,
                                int packetsize) {
   if (packetsize % int(sizeof(long)) != 0) {
@@ -216,13 +243,19 @@ void jerasure_bitmatrix_encode(int k, int m, int w, int* bitmatrix, char** data,
                  packetsize, w);
     std::exit(1);
   }
-  for (int i = 0; i < m; ++i)
-    jerasure_bitmatrix_dotprod(k, w, bitmatrix + size_t(i) * k * w * w, nullptr, k + i, data, coding, size,
-                               packetsize);
+  ecgpu_cpu::gpu_check("jerasure_bitmatrix_encode",
+                       ecgpu_jerasure_bitmatrix_encode(k, m, w, bitmatrix, data, coding, size, packetsize));
 }
 
 int jerasure_bitmatrix_decode(int k, int m, int w, int* bitmatrix, int row_k_ones, int* erasures, char** data,
                               char** coding, int size, int packetsize) {
+  if (w > 0 && packetsize > 0 && size % (w * packetsize) == 0) {
+    const int rc = ecgpu_jerasure_bitmatrix_decode(k, m, w, bitmatrix, row_k_ones, erasures, data, coding, size,
+                                                   packetsize);
+    if (rc == ECGPU_ERR) return -1;
+    ecgpu_cpu::gpu_check("jerasure_bitmatrix_decode", rc);
+    return 0;
+  }
   int* erased = ecgpu::erasures_to_erased(k, m, erasures);
   if (!erased) return -1;
   int edd = 0, lastdrive = k;
@@ -244,17 +277,17 @@ int jerasure_bitmatrix_decode(int k, int m, int w, int* bitmatrix, int row_k_one
   }
   for (int i = 0; edd > 0 && i < lastdrive; ++i)
     if (erased[i]) {
-      jerasure_bitmatrix_dotprod(k, w, dm.data() + i * blk, ids.data(), i, data, coding, size, packetsize);
+      cpu_bitmatrix_dotprod(k, w, dm.data() + i * blk, ids.data(), i, data, coding, size, packetsize);
       --edd;
     }
   if (edd > 0) {
     std::vector<int> t(static_cast<size_t>(k));
     for (int i = 0; i < k; ++i) t[i] = i < lastdrive ? i : i + 1;
-    jerasure_bitmatrix_dotprod(k, w, bitmatrix, t.data(), lastdrive, data, coding, size, packetsize);
+    cpu_bitmatrix_dotprod(k, w, bitmatrix, t.data(), lastdrive, data, coding, size, packetsize);
   }
   for (int i = 0; i < m; ++i)
     if (erased[k + i])
-      jerasure_bitmatrix_dotprod(k, w, bitmatrix + i * blk, nullptr, k + i, data, coding, size, packetsize);
+      cpu_bitmatrix_dotprod(k, w, bitmatrix + i * blk, nullptr, k + i, data, coding, size, packetsize);
   std::free(erased);
   return 0;
 }
@@ -368,6 +401,14 @@ void jerasure_free_schedule(int** schedule) {
 }
 
 void jerasure_do_scheduled_operations(char** ptrs, int** ops, int packetsize) {
+  ecgpu_cpu::gpu_check("jerasure_do_scheduled_operations",
+                       ecgpu_jerasure_do_scheduled_operations(ptrs, ops, packetsize));
+}
+
+namespace {
+// CPU form, for schedules over a size that is not whole super-packets (the
+// reference's loop then runs past the regions).
+void cpu_scheduled_operations(char** ptrs, int** ops, int packetsize) {
   for (int i = 0; ops[i][0] >= 0; ++i) {
     const int* o = ops[i];
     char* s = ptrs[o[0]] + o[1] * packetsize;
@@ -382,13 +423,20 @@ void jerasure_do_scheduled_operations(char** ptrs, int** ops, int packetsize) {
   }
 }
 
+}  // namespace
+
 void jerasure_schedule_encode(int k, int m, int w, int** schedule, char** data, char** coding, int size,
                               int packetsize) {
+  if (w > 0 && packetsize > 0 && size % (w * packetsize) == 0) {
+    ecgpu_cpu::gpu_check("jerasure_schedule_encode",
+                         ecgpu_jerasure_schedule_encode(k, m, w, schedule, data, coding, size, packetsize));
+    return;
+  }
   std::vector<char*> p(static_cast<size_t>(k + m));
   for (int i = 0; i < k; ++i) p[i] = data[i];
   for (int i = 0; i < m; ++i) p[k + i] = coding[i];
   for (int done = 0; done < size; done += packetsize * w) {
-    jerasure_do_scheduled_operations(p.data(), schedule, packetsize);
+    cpu_scheduled_operations(p.data(), schedule, packetsize);
     for (auto& q : p) q += packetsize * w;
   }
 }
@@ -489,8 +537,12 @@ int** decoding_schedule(int k, int m, int w, const int* bitmatrix, const int* er
 }
 
 void run_schedule(int k, int m, int w, int** schedule, char** ptrs, int size, int packetsize) {
+  if (w > 0 && packetsize > 0 && size % (w * packetsize) == 0) {
+    ecgpu_cpu::gpu_check("jerasure_schedule_decode", ecgpu_schedule_run(k + m, ptrs, schedule, w, size, packetsize));
+    return;
+  }
   for (int done = 0; done < size; done += packetsize * w) {
-    jerasure_do_scheduled_operations(ptrs, schedule, packetsize);
+    cpu_scheduled_operations(ptrs, schedule, packetsize);
     for (int i = 0; i < k + m; ++i)
       if (ptrs[i]) ptrs[i] += packetsize * w;
   }

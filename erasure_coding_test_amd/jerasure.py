@@ -107,3 +107,98 @@ def decode_plan(k: int, m: int, matrix, erasures, row_k_ones: int = 0):
     N.check(rc, "ecgpu_decode_plan")
     no, ns = n_out.value, n_src.value
     return (list(out_ids)[:no], list(src_ids)[:ns], [list(coefs[r * ns:(r + 1) * ns]) for r in range(no)])
+
+
+# ------------------------------------------------ GF(2) bit-matrix coding ----
+# jerasure.cpp:257-345, :623-703, :1034-1124, :1153-1192, :1346-1363.  The
+# matrices are host math; encode / decode / schedules execute on the MI355X as
+# one fused GF(2) packet map per call (size must be whole super-packets,
+# size % (w * packetsize) == 0).  A schedule is a list of 5-tuples
+# (src device, src packet, dst device, dst packet, xor?) -- the reference's
+# int** operations without the -1 terminator.
+
+def jerasure_matrix_to_bitmatrix(k: int, m: int, w: int, matrix) -> Optional[List[int]]:
+    return N.take_int_matrix(N.lib.ecgpu_jerasure_matrix_to_bitmatrix(k, m, w, N.int_array(matrix)),
+                             k * m * w * w)
+
+
+def jerasure_make_decoding_bitmatrix(k: int, m: int, w: int, matrix, erased) -> Tuple[int, List[int], List[int]]:
+    n = k * w * k * w
+    dm, ids = (N.c_int * n)(), (N.c_int * k)()
+    rc = N.lib.ecgpu_jerasure_make_decoding_bitmatrix(k, m, w, N.int_array(matrix), N.int_array(erased), dm, ids)
+    return rc, list(dm), list(ids)
+
+
+def jerasure_invert_bitmatrix(mat, rows: int) -> Tuple[int, List[int]]:
+    inv = (N.c_int * (rows * rows))()
+    return N.lib.ecgpu_jerasure_invert_bitmatrix(N.int_array(mat), inv, rows), list(inv)
+
+
+def jerasure_invertible_bitmatrix(mat, rows: int) -> int:
+    return N.lib.ecgpu_jerasure_invertible_bitmatrix(N.int_array(mat), rows)
+
+
+def _check_packets(fn: str, size: int, w: int, packetsize: int) -> None:
+    if packetsize <= 0 or size % (w * packetsize):
+        raise ValueError(f"{fn}: size % (w*packetsize) must be 0")
+
+
+def jerasure_bitmatrix_dotprod(k: int, w: int, bitmatrix_row, src_ids: Optional[Sequence[int]], dest_id: int,
+                               data_ptrs, coding_ptrs, size: int, packetsize: int) -> None:
+    _check_packets("jerasure_bitmatrix_dotprod", size, w, packetsize)
+    ids = None if src_ids is None else N.int_array(src_ids)
+    N.check(N.lib.ecgpu_jerasure_bitmatrix_dotprod(k, w, N.int_array(bitmatrix_row), ids, dest_id,
+                                                   N.ptr_array(addrs(data_ptrs)), N.ptr_array(addrs(coding_ptrs)),
+                                                   size, packetsize), "jerasure_bitmatrix_dotprod")
+
+
+def jerasure_bitmatrix_encode(k: int, m: int, w: int, bitmatrix, data_ptrs, coding_ptrs, size: int,
+                              packetsize: int) -> None:
+    _check_packets("jerasure_bitmatrix_encode", size, w, packetsize)
+    N.check(N.lib.ecgpu_jerasure_bitmatrix_encode(k, m, w, N.int_array(bitmatrix), N.ptr_array(addrs(data_ptrs)),
+                                                  N.ptr_array(addrs(coding_ptrs)), size, packetsize),
+            "jerasure_bitmatrix_encode")
+
+
+def jerasure_bitmatrix_decode(k: int, m: int, w: int, bitmatrix, row_k_ones: int, erasures, data_ptrs, coding_ptrs,
+                              size: int, packetsize: int) -> int:
+    _check_packets("jerasure_bitmatrix_decode", size, w, packetsize)
+    rc = N.lib.ecgpu_jerasure_bitmatrix_decode(k, m, w, N.int_array(bitmatrix), row_k_ones,
+                                               N.int_array(_erasure_list(erasures)), N.ptr_array(addrs(data_ptrs)),
+                                               N.ptr_array(addrs(coding_ptrs)), size, packetsize)
+    return N.check(rc, "jerasure_bitmatrix_decode")
+
+
+class _Schedule:
+    """A schedule as the reference's int** (malloc-free: ctypes-owned rows)."""
+
+    def __init__(self, ops):
+        self.rows = [(N.c_int * 5)(*op) for op in ops] + [(N.c_int * 5)(-1, 0, 0, 0, 0)]
+        self.table = (N.c_void_p * len(self.rows))(*[N.ctypes.addressof(r) for r in self.rows])
+
+
+def jerasure_do_scheduled_operations(ptrs, operations, packetsize: int) -> None:
+    sched = _Schedule(operations)
+    N.check(N.lib.ecgpu_jerasure_do_scheduled_operations(N.ptr_array(addrs(ptrs)), sched.table, packetsize),
+            "jerasure_do_scheduled_operations")
+
+
+def jerasure_schedule_encode(k: int, m: int, w: int, schedule, data_ptrs, coding_ptrs, size: int,
+                             packetsize: int) -> None:
+    _check_packets("jerasure_schedule_encode", size, w, packetsize)
+    sched = _Schedule(schedule)
+    N.check(N.lib.ecgpu_jerasure_schedule_encode(k, m, w, sched.table, N.ptr_array(addrs(data_ptrs)),
+                                                 N.ptr_array(addrs(coding_ptrs)), size, packetsize),
+            "jerasure_schedule_encode")
+
+
+def jerasure_dumb_bitmatrix_to_schedule(k: int, m: int, w: int, bitmatrix) -> List[Tuple[int, int, int, int, int]]:
+    """jerasure.cpp:1194-1224: one copy then XORs per output packet row."""
+    ops, cols = [], k * w
+    for r in range(m * w):
+        first = True
+        for c in range(cols):
+            if bitmatrix[r * cols + c]:
+                ops.append((c // w, c % w, k + r // w, r % w, 0 if first else 1))
+                first = False
+    return ops

@@ -74,6 +74,11 @@ ECGPU_API int* ecgpu_jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, 
 ECGPU_API int* ecgpu_jerasure_erasures_to_erased(int k, int m, int* erasures);           /* jerasure.cpp:507-532 */
 ECGPU_API int ecgpu_jerasure_make_decoding_matrix(int k, int m, int w, int* matrix, int* erased,
                                                   int* decoding_matrix, int* dm_ids);    /* jerasure.cpp:84-112  */
+ECGPU_API int* ecgpu_jerasure_matrix_to_bitmatrix(int k, int m, int w, int* matrix);      /* jerasure.cpp:257-283 */
+ECGPU_API int ecgpu_jerasure_make_decoding_bitmatrix(int k, int m, int w, int* matrix, int* erased,
+                                                     int* decoding_matrix, int* dm_ids); /* jerasure.cpp:115-151 */
+ECGPU_API int ecgpu_jerasure_invert_bitmatrix(int* mat, int* inv, int rows);              /* jerasure.cpp:1034-1089 */
+ECGPU_API int ecgpu_jerasure_invertible_bitmatrix(int* mat, int rows);                    /* jerasure.cpp:1091-1124 */
 
 /* Fused decode plan (host only): the single linear map that
  * jerasure_matrix_decode (jerasure.cpp:153-254) applies, over shard ids
@@ -109,6 +114,23 @@ ECGPU_API int ecgpu_reed_sol_r6_encode(int k, int w, char** data_ptrs, char** co
 ECGPU_API int ecgpu_reed_sol_galois_w08_region_multby_2(char* region, int nbytes);
 ECGPU_API int ecgpu_reed_sol_galois_w16_region_multby_2(char* region, int nbytes);
 ECGPU_API int ecgpu_reed_sol_galois_w32_region_multby_2(char* region, int nbytes);
+/* GF(2) packet coding on the GPU: a device is w packets of packetsize bytes
+ * per super-packet (size % (w*packetsize) must be 0, else ECGPU_ERR_ARG).
+ * jerasure.cpp:301-345, :1346-1363, :623-703 (0 / -1 like the reference). */
+ECGPU_API int ecgpu_jerasure_bitmatrix_dotprod(int k, int w, int* bitmatrix_row, int* src_ids, int dest_id,
+                                               char** data_ptrs, char** coding_ptrs, int size, int packetsize);
+ECGPU_API int ecgpu_jerasure_bitmatrix_encode(int k, int m, int w, int* bitmatrix, char** data_ptrs,
+                                              char** coding_ptrs, int size, int packetsize);
+ECGPU_API int ecgpu_jerasure_bitmatrix_decode(int k, int m, int w, int* bitmatrix, int row_k_ones, int* erasures,
+                                              char** data_ptrs, char** coding_ptrs, int size, int packetsize);
+/* jerasure.cpp:1153-1176 (one super-packet at ptrs) and :1178-1192 */
+ECGPU_API int ecgpu_jerasure_do_scheduled_operations(char** ptrs, int** operations, int packetsize);
+ECGPU_API int ecgpu_jerasure_schedule_encode(int k, int m, int w, int** schedule, char** data_ptrs, char** coding_ptrs,
+                                             int size, int packetsize);
+/* A schedule over size/(w*packetsize) super-packets of nptrs devices (NULL
+ * where unused): the engine behind schedule_encode and the scheduled decodes
+ * (jerasure.cpp:935-995, whose schedules are built on the host). */
+ECGPU_API int ecgpu_schedule_run(int nptrs, char** ptrs, int** operations, int w, int size, int packetsize);
 /* jerasure.cpp:1143-1151: fills xor, gf, memcpy byte counts and resets. */
 ECGPU_API int ecgpu_jerasure_get_stats(double* fill_in);
 

@@ -620,3 +620,72 @@ def test_wide_word_region_ops_device(ec, gpu, w):
     two = np.array([ec.galois.galois_single_multiply(int(x), 2, w) & 0xFFFFFFFF for x in sw], dtype=sw.dtype)
     assert np.array_equal(ts.cpu().numpy().view(sw.dtype), two)
     assert W in (2, 4)
+
+
+# ------------------------------------------ GF(2) bit-matrix / schedules ----
+def _np_bitmatrix_encode(k, m, w, bm, data, size, ps):
+    """Plain numpy restatement of jerasure_bitmatrix_encode (jerasure.cpp:301-345)."""
+    out = [np.zeros(size, np.uint8) for _ in range(m)]
+    for i in range(m):
+        for sp in range(0, size, w * ps):
+            for j in range(w):
+                acc = np.zeros(ps, np.uint8)
+                row = bm[(i * w + j) * k * w:(i * w + j + 1) * k * w]
+                for x in range(k):
+                    for y in range(w):
+                        if row[x * w + y]:
+                            acc ^= data[x][sp + y * ps:sp + (y + 1) * ps]
+                out[i][sp + j * ps:sp + (j + 1) * ps] = acc
+    return out
+
+
+@pytest.mark.parametrize("k,m,w,ps", [(10, 4, 8, 2048), (6, 5, 8, 512), (4, 2, 16, 256)])
+def test_bitmatrix_coding_device(ec, gpu, k, m, w, ps):
+    """Device tensors through the Python mirror: bit-matrix encode (>32 output
+    packet rows for m=5: two launches), dumb-schedule encode, and decode."""
+    import torch
+    J = ec.jerasure
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w)
+    bm = J.jerasure_matrix_to_bitmatrix(k, m, w, M)
+    size = w * ps * 6
+    rng = np.random.default_rng(k * 1000 + ps)
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)]
+    want = _np_bitmatrix_encode(k, m, w, bm, data, size, ps)
+    dd = [torch.from_numpy(a).to(gpu) for a in data]
+    dc = [torch.zeros(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    J.jerasure_bitmatrix_encode(k, m, w, bm, dd, dc, size, ps)
+    torch.cuda.synchronize()
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), want[i]), i
+    dc2 = [torch.zeros(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    J.jerasure_schedule_encode(k, m, w, J.jerasure_dumb_bitmatrix_to_schedule(k, m, w, bm), dd, dc2, size, ps)
+    torch.cuda.synchronize()
+    for i in range(m):
+        assert torch.equal(dc[i], dc2[i]), i
+    er = [0, k - 1, k + m - 1][: m]
+    for e in er:
+        (dd + dc)[e].fill_(0x33)
+    assert J.jerasure_bitmatrix_decode(k, m, w, bm, 1, er, dd, dc, size, ps) == 0
+    torch.cuda.synchronize()
+    for j in range(k):
+        assert np.array_equal(dd[j].cpu().numpy(), data[j]), j
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), want[i]), i
+
+
+def test_scheduled_operations_accumulate_many_rows(ec, gpu):
+    """XOR-into-destination ops (the destination's old content is a source)
+    over 40 output packets: more rows than one launch, outputs via temps."""
+    ps, npk = 64, 40
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 256, npk * ps, dtype=np.uint8)
+    b = rng.integers(0, 256, npk * ps, dtype=np.uint8)
+    ops = [(0, p, 1, p, 1) for p in range(npk)] + [(1, p, 1, (p + 1) % npk, 1) for p in range(npk)]
+    want_b = b.copy().reshape(npk, ps)
+    av = a.reshape(npk, ps)
+    for p in range(npk):
+        want_b[p] ^= av[p]
+    for p in range(npk):
+        want_b[(p + 1) % npk] ^= want_b[p]
+    ec.jerasure.jerasure_do_scheduled_operations([a, b], ops, ps)
+    assert np.array_equal(b.reshape(npk, ps), want_b)

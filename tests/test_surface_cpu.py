@@ -209,18 +209,36 @@ def read_schedule(addr):
         i += 1
 
 
-@pytest.mark.parametrize("k,m,w", [(4, 2, 8), (6, 3, 8), (5, 2, 4), (3, 3, 8)])
-def test_bitmatrix_and_schedules(libs, k, m, w):
+BM_CASES = [(4, 2, 8), (6, 3, 8), (5, 2, 4), (3, 3, 8)]
+
+
+def _bitmatrices(libs, k, m, w):
     ref, mine = libs
     M = list(np.ctypeslib.as_array(ctypes.cast(ref.vdm(k, m, w), IP), shape=(k * m,)))
-    bm_ref = ref.to_bitmatrix(k, m, w, ints(M))
-    bm_mine = mine.to_bitmatrix(k, m, w, ints(M))
+    return ref.to_bitmatrix(k, m, w, ints(M)), mine.to_bitmatrix(k, m, w, ints(M))
+
+
+@pytest.mark.parametrize("k,m,w", BM_CASES)
+def test_bitmatrix_and_schedule_construction(libs, k, m, w):
+    """Host half: bit-matrices and dumb / smart schedules are identical."""
+    ref, mine = libs
+    bm_ref, bm_mine = _bitmatrices(libs, k, m, w)
     n = k * m * w * w
     assert np.array_equal(np.ctypeslib.as_array(ctypes.cast(bm_ref, IP), shape=(n,)),
                           np.ctypeslib.as_array(ctypes.cast(bm_mine, IP), shape=(n,)))
     for kind in ("dumb", "smart"):
         assert read_schedule(getattr(ref, kind)(k, m, w, bm_ref)) == read_schedule(getattr(mine, kind)(k, m, w, bm_mine))
-    ps = 64
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ps", [64, 1000, 4096])
+@pytest.mark.parametrize("k,m,w", BM_CASES)
+def test_bitmatrix_and_schedule_coding(libs, k, m, w, ps):
+    """Execution on the MI355X (GF(2) packet kernels; ps = 1000 takes the
+    byte kernel): bit-matrix encode / decode, scheduled encode, lazy and
+    cached scheduled decode, and the byte counters, against the reference."""
+    ref, mine = libs
+    bm_ref, bm_mine = _bitmatrices(libs, k, m, w)
     size = w * ps * 3
     rng = np.random.default_rng(k * 100 + m)
     data = rand_bufs(rng, k, size)

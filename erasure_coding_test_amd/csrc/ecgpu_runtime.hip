@@ -1052,12 +1052,9 @@ ECGPU_API int ecgpu_reed_sol_r6_encode(int k, int w, char** data_ptrs, char** co
 // super-packet (gf_xor_packets).
 namespace {
 
-constexpr int kRowBits = 20;
-inline void* pkey(int slot, int row) {
-  return reinterpret_cast<void*>(((uintptr_t(slot) << kRowBits) | uintptr_t(row)) + 1);
-}
-inline int pslot(const void* k) { return int((reinterpret_cast<uintptr_t>(k) - 1) >> kRowBits); }
-inline int prow(const void* k) { return int((reinterpret_cast<uintptr_t>(k) - 1) & ((1u << kRowBits) - 1)); }
+inline int pslot(const void* k) { return PacketTracker::key_slot(k); }
+inline int prow(const void* k) { return PacketTracker::key_row(k); }
+constexpr int kMaxPacketRow = (1 << 20) - 1;
 
 constexpr int kPacketRows = 32;  // output packet rows per launch (uint32 masks)
 
@@ -1134,14 +1131,16 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
   for (int r = 0; r < rows; ++r)
     for (int j = 0; j < nsrc; ++j)
       if (op.coef[size_t(r) * nsrc + j]) masks[size_t(r / kPacketRows) * nsrc + j] |= 1u << (r % kPacketRows);
+  // one upload of [src bases | dst bases | masks]
+  std::vector<uint8_t> host_tab(tab_bytes);
+  std::memcpy(host_tab.data(), sb.data(), sizeof(void*) * nsrc);
+  std::memcpy(host_tab.data() + sizeof(void*) * nsrc, db.data(), sizeof(void*) * rows);
+  std::memcpy(host_tab.data() + sizeof(void*) * size_t(nsrc + rows), masks.data(), masks.size() * sizeof(uint32_t));
   uint8_t* tab = c->stage + tab_off;
   auto* d_src = reinterpret_cast<const uint8_t**>(tab);
   auto* d_dst = reinterpret_cast<uint8_t**>(tab + sizeof(void*) * nsrc);
   auto* d_mask = reinterpret_cast<uint32_t*>(tab + sizeof(void*) * size_t(nsrc + rows));
-  if (nsrc) ECGPU_HIP(hipMemcpyAsync(d_src, sb.data(), sizeof(void*) * nsrc, hipMemcpyHostToDevice, c->stream));
-  ECGPU_HIP(hipMemcpyAsync(d_dst, db.data(), sizeof(void*) * rows, hipMemcpyHostToDevice, c->stream));
-  if (nsrc)
-    ECGPU_HIP(hipMemcpyAsync(d_mask, masks.data(), masks.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+  ECGPU_HIP(hipMemcpyAsync(tab, host_tab.data(), tab_bytes, hipMemcpyHostToDevice, c->stream));
 
   const int64_t dstride = via_temp ? ps : spstride;
   bool aligned = ps % 8 == 0 && spstride % 8 == 0 && dstride % 8 == 0;
@@ -1190,22 +1189,21 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
 
 // jerasure_bitmatrix_dotprod (jerasure.cpp:301-345) for ONE super-packet on
 // virtual packet rows; byte counters scaled by the super-packet count.
-void record_bitmatrix_dotprod(LinearTracker& t, int k, int w, const int* row, const int* src_ids, int dest_id,
+void record_bitmatrix_dotprod(PacketTracker& t, int k, int w, const int* row, const int* src_ids, int dest_id,
                               int64_t ps, int64_t nsp) {
   int index = 0;
   for (int j = 0; j < w; ++j) {
     bool started = false;
-    void* dst = pkey(dest_id, j);
     for (int x = 0; x < k; ++x) {
       const int dev = src_ids ? src_ids[x] : x;
       for (int y = 0; y < w; ++y, ++index) {
         if (!row[index]) continue;
         if (!started) {
-          t.copy(dst, pkey(dev, y));
+          t.copy(dest_id, j, dev, y);
           t.count(0, 0, double(ps) * double(nsp));
           started = true;
         } else {
-          t.xor3(dst, pkey(dev, y), dst);
+          t.xor_into(dest_id, j, dev, y);
           t.count(double(ps) * double(nsp), 0, 0);
         }
       }
@@ -1219,24 +1217,33 @@ std::vector<char*> device_ptrs(int k, int n, char** data, char** coding) {
   return p;
 }
 
-// Replays a schedule (ops[i] = {src dev, src packet, dst dev, dst packet, xor?},
-// terminated by ops[i][0] < 0) for one super-packet.
-int record_schedule(LinearTracker& t, int** ops, int64_t ps, int64_t nsp, int* max_dev) {
+// Devices and packet rows a schedule names (ops[i] = {src dev, src packet,
+// dst dev, dst packet, xor?}, terminated by ops[i][0] < 0).
+int schedule_extent(int** ops, int* max_dev, int* max_row) {
   *max_dev = -1;
+  *max_row = -1;
   for (int i = 0; ops[i][0] >= 0; ++i) {
     const int* o = ops[i];
-    if (o[1] < 0 || o[3] < 0 || o[1] >= (1 << kRowBits) || o[3] >= (1 << kRowBits) || o[2] < 0)
+    if (o[1] < 0 || o[3] < 0 || o[1] > kMaxPacketRow || o[3] > kMaxPacketRow || o[2] < 0)
       return fail(ECGPU_ERR_ARG, "schedule op out of range");
-    if (o[4]) {
-      t.xor3(pkey(o[0], o[1]), pkey(o[2], o[3]), pkey(o[2], o[3]));
-      t.count(double(ps) * double(nsp), 0, 0);
-    } else {
-      t.copy(pkey(o[2], o[3]), pkey(o[0], o[1]));
-      t.count(0, 0, double(ps) * double(nsp));
-    }
     *max_dev = std::max(*max_dev, std::max(o[0], o[2]));
+    *max_row = std::max(*max_row, std::max(o[1], o[3]));
   }
   return ECGPU_OK;
+}
+
+// Replays a schedule for one super-packet.
+void record_schedule(PacketTracker& t, int** ops, int64_t ps, int64_t nsp) {
+  for (int i = 0; ops[i][0] >= 0; ++i) {
+    const int* o = ops[i];
+    if (o[4]) {
+      t.xor_into(o[2], o[3], o[0], o[1]);
+      t.count(double(ps) * double(nsp), 0, 0);
+    } else {
+      t.copy(o[2], o[3], o[0], o[1]);
+      t.count(0, 0, double(ps) * double(nsp));
+    }
+  }
 }
 
 }  // namespace
@@ -1251,7 +1258,7 @@ ECGPU_API int ecgpu_jerasure_bitmatrix_dotprod(int k, int w, int* bitmatrix_row,
   int n = std::max(k, dest_id + 1);
   if (src_ids)
     for (int x = 0; x < k; ++x) n = std::max(n, src_ids[x] + 1);
-  LinearTracker t;
+  PacketTracker t(n, w);
   record_bitmatrix_dotprod(t, k, w, bitmatrix_row, src_ids, dest_id, packetsize, nsp);
   // ids >= k index coding_ptrs; only the ids the op touches are dereferenced
   std::vector<char*> p(static_cast<size_t>(n), nullptr);
@@ -1266,7 +1273,7 @@ ECGPU_API int ecgpu_jerasure_bitmatrix_encode(int k, int m, int w, int* bitmatri
   if (k <= 0 || m <= 0 || w <= 0 || packetsize <= 0 || !bitmatrix || size % (w * packetsize) != 0)
     return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_bitmatrix_encode: size % (packetsize*w) must be 0");
   const int64_t nsp = size / (int64_t(w) * packetsize);
-  LinearTracker t;
+  PacketTracker t(k + m, w);
   for (int i = 0; i < m; ++i)
     record_bitmatrix_dotprod(t, k, w, bitmatrix + size_t(i) * k * w * w, nullptr, k + i, packetsize, nsp);
   return execute_packets(t.finish(), device_ptrs(k, k + m, data_ptrs, coding_ptrs), nsp, int64_t(w) * packetsize,
@@ -1298,7 +1305,7 @@ ECGPU_API int ecgpu_jerasure_bitmatrix_decode(int k, int m, int w, int* bitmatri
       return ECGPU_ERR;
     }
   }
-  LinearTracker t;
+  PacketTracker t(k + m, w);
   for (int i = 0; edd > 0 && i < lastdrive; ++i)
     if (erased[i]) {
       record_bitmatrix_dotprod(t, k, w, dm.data() + i * blk, ids.data(), i, packetsize, nsp);
@@ -1320,9 +1327,11 @@ ECGPU_API int ecgpu_jerasure_bitmatrix_decode(int k, int m, int w, int* bitmatri
 ECGPU_API int ecgpu_jerasure_do_scheduled_operations(char** ptrs, int** operations, int packetsize) {
   if (!ptrs || !operations || packetsize <= 0)
     return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_do_scheduled_operations: bad arguments");
-  LinearTracker t;
-  int max_dev = -1;
-  if (int rc = record_schedule(t, operations, packetsize, 1, &max_dev)) return rc;
+  int max_dev = -1, max_row = -1;
+  if (int rc = schedule_extent(operations, &max_dev, &max_row)) return rc;
+  if (max_dev < 0) return ECGPU_OK;
+  PacketTracker t(max_dev + 1, max_row + 1);
+  record_schedule(t, operations, packetsize, 1);
   std::vector<char*> p(ptrs, ptrs + (max_dev + 1));
   return execute_packets(t.finish(), p, 1, 0, packetsize);
 }
@@ -1333,10 +1342,12 @@ ECGPU_API int ecgpu_schedule_run(int nptrs, char** ptrs, int** operations, int w
   if (nptrs <= 0 || !ptrs || !operations || w <= 0 || packetsize <= 0 || size % (w * packetsize) != 0)
     return fail(ECGPU_ERR_ARG, "ecgpu_schedule_run: size % (w*packetsize) must be 0");
   const int64_t nsp = size / (int64_t(w) * packetsize);
-  LinearTracker t;
-  int max_dev = -1;
-  if (int rc = record_schedule(t, operations, packetsize, nsp, &max_dev)) return rc;
+  int max_dev = -1, max_row = -1;
+  if (int rc = schedule_extent(operations, &max_dev, &max_row)) return rc;
   if (max_dev >= nptrs) return fail(ECGPU_ERR_ARG, "ecgpu_schedule_run: schedule names a device >= nptrs");
+  if (max_dev < 0) return ECGPU_OK;
+  PacketTracker t(max_dev + 1, max_row + 1);
+  record_schedule(t, operations, packetsize, nsp);
   std::vector<char*> p(ptrs, ptrs + nptrs);
   return execute_packets(t.finish(), p, nsp, int64_t(w) * packetsize, packetsize);
 }

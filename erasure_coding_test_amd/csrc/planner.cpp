@@ -27,19 +27,30 @@ LinearTracker::Vec& LinearTracker::state(int b) {
   return v;
 }
 
+// All ids are registered before any state reference is taken: id() may grow
+// state_, which would invalidate the references.  Ops update the destination
+// in place (no temporaries): schedules replay thousands of them per call.
 void LinearTracker::copy(void* dst, void* src) {
   const int d = id(dst), s = id(src);
-  Vec v = state(s);
-  state(d) = std::move(v);
+  if (d == s) return;
+  const Vec& v = state(s);
+  state(d) = v;  // copy-assign reuses the destination's capacity
   written_[d] = 1;
 }
 
 void LinearTracker::xor3(void* r1, void* r2, void* r3) {
   const int a = id(r1), b = id(r2), c = id(r3);
-  Vec v = state(a);
-  const Vec& w = state(b);
-  for (size_t i = 0; i < v.size(); ++i) v[i] ^= w[i];
-  state(c) = std::move(v);
+  const size_t n = bufs_.size();
+  Vec& dst = state(c);
+  int other = b;  // the operand not already in dst
+  if (c == b && c != a) {
+    other = a;
+  } else if (c != a) {
+    dst = state(a);
+  }
+  const Vec& o = state(other);
+  dst.resize(n, 0);
+  for (size_t i = 0; i < n && i < o.size(); ++i) dst[i] ^= o[i];
   written_[c] = 1;
 }
 
@@ -121,6 +132,78 @@ FusedOp LinearTracker::finish() const {
     if (col[outs[r]] >= 0) op.dst_is_src = true;
   }
   op.w = w_;
+  op.xor_bytes = xor_;
+  op.gf_bytes = gf_;
+  op.memcpy_bytes = memcpy_;
+  return op;
+}
+
+// ------------------------------------------------------- PacketTracker ----
+namespace {
+constexpr int kRowBits = 20;
+}
+
+void* PacketTracker::packet_key(int slot, int row) {
+  return reinterpret_cast<void*>(((uintptr_t(slot) << kRowBits) | uintptr_t(row)) + 1);
+}
+int PacketTracker::key_slot(const void* key) { return int((reinterpret_cast<uintptr_t>(key) - 1) >> kRowBits); }
+int PacketTracker::key_row(const void* key) {
+  return int((reinterpret_cast<uintptr_t>(key) - 1) & ((uintptr_t(1) << kRowBits) - 1));
+}
+
+PacketTracker::PacketTracker(int nslots, int nrows)
+    : nslots_(nslots), nrows_(nrows), n_(nslots * nrows), words_((nslots * nrows + 63) / 64) {
+  bits_.assign(size_t(n_) * size_t(words_), 0);
+  for (int b = 0; b < n_; ++b) bits_[size_t(b) * words_ + size_t(b / 64)] |= uint64_t(1) << (b % 64);
+  written_.assign(size_t(n_), 0);
+}
+
+void PacketTracker::copy(int dslot, int drow, int sslot, int srow) {
+  const int d = idx(dslot, drow), s = idx(sslot, srow);
+  if (d != s)
+    for (int i = 0; i < words_; ++i) bits_[size_t(d) * words_ + i] = bits_[size_t(s) * words_ + i];
+  written_[size_t(d)] = 1;
+}
+
+void PacketTracker::xor_into(int dslot, int drow, int sslot, int srow) {
+  const int d = idx(dslot, drow), s = idx(sslot, srow);
+  for (int i = 0; i < words_; ++i) bits_[size_t(d) * words_ + i] ^= bits_[size_t(s) * words_ + i];
+  written_[size_t(d)] = 1;
+}
+
+FusedOp PacketTracker::finish() const {
+  FusedOp op;
+  op.w = 1;
+  auto for_bits = [&](int b, auto&& fn) {  // every set bit of state b, ascending
+    const uint64_t* v = &bits_[size_t(b) * words_];
+    for (int i = 0; i < words_; ++i)
+      for (uint64_t x = v[i]; x; x &= x - 1) fn(i * 64 + __builtin_ctzll(x));
+  };
+  std::vector<int> outs;
+  for (int b = 0; b < n_; ++b) {
+    if (!written_[size_t(b)]) continue;
+    const uint64_t* v = &bits_[size_t(b) * words_];
+    bool identity = true;
+    for (int i = 0; identity && i < words_; ++i)
+      identity = v[i] == ((b / 64 == i) ? (uint64_t(1) << (b % 64)) : 0);
+    if (!identity) outs.push_back(b);  // unchanged content needs no write
+  }
+  std::vector<int> col(size_t(n_), -1), src_of;
+  for (int b : outs)
+    for_bits(b, [&](int i) {
+      if (col[size_t(i)] < 0) {
+        col[size_t(i)] = int(src_of.size());
+        src_of.push_back(i);
+      }
+    });
+  for (int i : src_of) op.srcs.push_back(packet_key(i / nrows_, i % nrows_));
+  op.coef.assign(outs.size() * src_of.size(), 0);
+  for (size_t r = 0; r < outs.size(); ++r) {
+    const int b = outs[r];
+    for_bits(b, [&](int i) { op.coef[r * src_of.size() + size_t(col[size_t(i)])] = 1; });
+    op.dsts.push_back(packet_key(b / nrows_, b % nrows_));
+    if (col[size_t(b)] >= 0) op.dst_is_src = true;
+  }
   op.xor_bytes = xor_;
   op.gf_bytes = gf_;
   op.memcpy_bytes = memcpy_;

@@ -65,6 +65,35 @@ class LinearTracker {
   double xor_ = 0, gf_ = 0, memcpy_ = 0;
 };
 
+// GF(2) specialisation for packet coding (bit-matrices and schedules,
+// jerasure.cpp:301-345, :1153-1192): buffers are the dense "packet row r of
+// device slot s" (s < nslots, r < nrows), every coefficient is 0/1, so a
+// state is a bitset and an op is a few word XORs -- schedules replay
+// thousands of ops per call.  finish() returns the same FusedOp shape with
+// srcs / dsts holding packet keys (see packet_key) and 0/1 coefficients.
+class PacketTracker {
+ public:
+  PacketTracker(int nslots, int nrows);
+  void copy(int dslot, int drow, int sslot, int srow);  // dst = src
+  void xor_into(int dslot, int drow, int sslot, int srow);  // dst ^= src
+  void count(double xor_b, double gf_b, double memcpy_b) {
+    xor_ += xor_b;
+    gf_ += gf_b;
+    memcpy_ += memcpy_b;
+  }
+  FusedOp finish() const;
+  static void* packet_key(int slot, int row);
+  static int key_slot(const void* key);
+  static int key_row(const void* key);
+
+ private:
+  int idx(int slot, int row) const { return slot * nrows_ + row; }
+  int nslots_, nrows_, n_, words_;
+  std::vector<uint64_t> bits_;  // n_ states of words_ words each
+  std::vector<char> written_;
+  double xor_ = 0, gf_ = 0, memcpy_ = 0;
+};
+
 // jerasure_matrix_encode (jerasure.cpp:285-299) as a fused op, w = t.w().
 void plan_encode(LinearTracker& t, int k, int m, const int* matrix, char** data, char** coding, int64_t size);
 

@@ -7,6 +7,8 @@
 //   variant 2: gf_apply_lds<K, R> (north-star LDS nibble tables)
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "gf_kernels.hpp"
 
 using ecgpu::dev::ApplyArgs;
@@ -111,6 +113,10 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
     grid = dim3(unsigned(stripes), unsigned((a.nvec + 255) / 256));
   }
   void* args[] = {&a};
-  return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(256), args, 0,
+  // ECGPU_DIAG_LDS: dynamic LDS bytes per block, unused by the kernels -- caps
+  // resident blocks per CU at 160 KiB / bytes (occupancy experiments).
+  const char* lds_env = std::getenv("ECGPU_DIAG_LDS");
+  const unsigned lds = lds_env ? unsigned(std::atoi(lds_env)) : 0u;
+  return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(256), args, lds,
                          static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -3;
 }

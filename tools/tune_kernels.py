@@ -55,12 +55,22 @@ def main():
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--stripes", type=int, default=24)
     ap.add_argument("--pads", default="0", help="comma list of per-shard padding bytes (shard stride = S + pad)")
+    ap.add_argument("--lds", default="", help="comma list of dynamic LDS bytes per block (occupancy caps); "
+                    "each value runs the variants again under ECGPU_DIAG_LDS")
     ap.add_argument("--only", default="", help="comma list of substrings; keep variants matching any")
     args = ap.parse_args()
     k, m, S, B = 10, 4, 4 << 20, args.stripes
     results = []
     for pad in [int(p) for p in args.pads.split(",")]:
-        results += run_layout(args, k, m, S, B, pad)
+        if args.lds:
+            for lds in args.lds.split(","):
+                os.environ["ECGPU_DIAG_LDS"] = lds
+                for r in run_layout(args, k, m, S, B, pad):
+                    r["lds"] = int(lds)
+                    results.append(r)
+            os.environ.pop("ECGPU_DIAG_LDS", None)
+        else:
+            results += run_layout(args, k, m, S, B, pad)
     for r in results:
         print(json.dumps(r))
 

@@ -78,6 +78,19 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
     if (K == 10 && R == 1)
       fn = vec == 1 ? &ecgpu::dev::gf_apply<10, 1, 4, 1>
                     : vec == 2 ? &ecgpu::dev::gf_apply<10, 1, 4, 2> : &ecgpu::dev::gf_apply<10, 1, 4, 4>;
+  } else if (variant == 9) {
+    // access-pattern probe: XOR-only gf_apply_perm over (K, R) shapes
+    vec = 1;
+    if (K == 1 && R == 1) fn = &ecgpu::dev::gf_apply_perm<1, 1, 1, 3>;
+    if (K == 2 && R == 2) fn = &ecgpu::dev::gf_apply_perm<2, 2, 1, 3>;
+    if (K == 4 && R == 4) fn = &ecgpu::dev::gf_apply_perm<4, 4, 1, 3>;
+    if (K == 7 && R == 7) fn = &ecgpu::dev::gf_apply_perm<7, 7, 1, 3>;
+    if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_perm<10, 4, 1, 3>;
+    if (K == 10 && R == 1) fn = &ecgpu::dev::gf_apply_perm<10, 1, 1, 3>;
+    if (K == 13 && R == 1) fn = &ecgpu::dev::gf_apply_perm<13, 1, 1, 3>;
+    if (K == 4 && R == 1) fn = &ecgpu::dev::gf_apply_perm<4, 1, 1, 3>;
+    if (K == 1 && R == 4) fn = &ecgpu::dev::gf_apply_perm<1, 4, 1, 3>;
+    if (K == 2 && R == 1) fn = &ecgpu::dev::gf_apply_perm<2, 1, 1, 3>;
   } else if (variant == 2) {
     vec = 1;
     if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_lds<10, 4>;

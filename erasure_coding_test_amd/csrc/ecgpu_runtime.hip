@@ -118,9 +118,31 @@ KernelFn generic_fn(int R) {
   }
 }
 
-hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t s) {
+hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t s, unsigned lds_bytes = 0) {
   void* args[] = {&a};
-  return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, block, args, 0, s);
+  return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, block, args, lds_bytes, s);
+}
+
+// Residency cap for the streaming kernels.  Fewer resident workgroups per CU
+// means fewer DRAM pages open at once across the chip: with each lane reading
+// K shards and writing R, the uncapped kernel (VGPR-limited to 7 blocks/CU)
+// keeps ~28k distinct 4 KiB shard chunks in flight and loses to row-buffer
+// thrash; 3 blocks/CU measured +8 % encode / +3 % decode on RS(10,4) 4 MiB
+// (profiles/r01_tune_occupancy.jsonl).  The cap is an unused
+// dynamic LDS allocation of LDS_per_CU / blocks (rounded down to 512 B).
+// ECGPU_BLOCKS_PER_CU overrides (0 = uncapped).
+unsigned residency_lds_bytes(int device) {
+  static std::once_flag once;
+  static int per_cu = 0;
+  static int blocks = 0;
+  std::call_once(once, [&] {
+    if (hipDeviceGetAttribute(&per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess)
+      per_cu = 0;
+    blocks = env_int("ECGPU_BLOCKS_PER_CU", 3);
+  });
+  if (blocks <= 0 || per_cu <= 0) return 0;
+  const unsigned b = unsigned(per_cu / blocks) & ~511u;
+  return b > unsigned(per_cu / (blocks + 1)) ? b : 0u;
 }
 
 // Per-coefficient tables.  PERM: word p holds c*(e << 2p) in byte e.  LDS:
@@ -379,7 +401,8 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
       if (nvec > 0) {
         const int64_t per_block = int64_t(dev::kBlock) * vec;
         const dim3 grid(unsigned((nvec + per_block - 1) / per_block), unsigned(ns));
-        ECGPU_HIP(launch(vec_fn, grid, block, a, stream));
+        const unsigned lds = p->kind == ECGPU_KERNEL_PERM ? residency_lds_bytes(p->device) : 0u;
+        ECGPU_HIP(launch(vec_fn, grid, block, a, stream, lds));
       }
       if (byte0 < p->size) {
         const dim3 grid(unsigned((p->size - byte0 + dev::kBlock - 1) / dev::kBlock), unsigned(ns));

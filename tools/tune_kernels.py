@@ -141,6 +141,11 @@ def run_layout(args, k, m, S, B, pad):
         variants.append((f"V dec1 vec{vec}", 8, 10, 1, vec, 4, qd, nd, src_dec, dst_dec, B, ud, zd,
                          (k + 1) * S * B, 1))
     only = [o for o in args.only.split(",")] if args.only else [""]
+    # access-pattern probe (XOR-only, per-lane K reads + R writes)
+    for K2, R2 in ((1, 1), (2, 1), (2, 2), (4, 1), (1, 4), (4, 4), (7, 7), (10, 1), (10, 4), (13, 1)):
+        st = ptr_table([addr(s, j) for s in range(B) for j in range(K2)])
+        dt = ptr_table([addr(s, K2 + i) for s in range(B) for i in range(R2)])
+        variants.append((f"P xor K{K2} R{R2}", 9, K2, R2, 1, 3, q_enc, n_enc, st, dt, B, 0, 0, (K2 + R2) * S * B, 1))
     variants = [v for v in variants if any(o in v[0] for o in only)]
     times = {v[0]: [] for v in variants}
     import random

@@ -127,10 +127,14 @@ hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t 
 // means fewer DRAM pages open at once across the chip: with each lane reading
 // K shards and writing R, the uncapped kernel (VGPR-limited to 7 blocks/CU)
 // keeps ~28k distinct 4 KiB shard chunks in flight and loses to row-buffer
-// thrash; 3 blocks/CU measured +8 % encode / +3 % decode on RS(10,4) 4 MiB
-// (profiles/r01_tune_occupancy.jsonl).  The cap is an unused
-// dynamic LDS allocation of LDS_per_CU / blocks (rounded down to 512 B).
-// ECGPU_BLOCKS_PER_CU overrides (0 = uncapped).
+// thrash.  3 blocks/CU measured (profiles/r01_residency_*.json):
+// RS(6,3) encode +21 %, RS(12,4) +6 %, RS(10,4) decode{0} +5 %, the bench
+// step +4.5 %; but a launch dense in GF multiplies (decode{0,1,2,3}: 40
+// non-unit coefficients over 14 shards) needs the occupancy to hide its VALU
+// work and loses 11 %, so launches with more than 2.5 multiply terms per
+// shard touched stay uncapped.  The cap is an unused dynamic LDS allocation
+// of LDS_per_CU / blocks (rounded down to 512 B).  ECGPU_BLOCKS_PER_CU
+// overrides the block count (0 = never cap).
 unsigned residency_lds_bytes(int device) {
   static std::once_flag once;
   static int per_cu = 0;
@@ -372,6 +376,10 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
     KernelFn vec_fn = spec ? SpecTable::get(p->kind == ECGPU_KERNEL_LDS, K, R, unit_variant(p->coef, K, r0, R))
                            : generic_fn(R);
     const int vec = 1;
+    int mul_terms = 0;  // coefficients that are neither 0 nor 1
+    for (int r = 0; r < R; ++r)
+      for (int j = 0; j < K; ++j) mul_terms += p->coef[size_t(r0 + r) * K + j] > 1u;
+    const bool cap = p->kind == ECGPU_KERNEL_PERM && 2 * mul_terms <= 5 * (K + R);
     uint64_t unit = 0, zero = 0;
     if (spec)
       for (int r = 0; r < R; ++r)
@@ -401,7 +409,7 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
       if (nvec > 0) {
         const int64_t per_block = int64_t(dev::kBlock) * vec;
         const dim3 grid(unsigned((nvec + per_block - 1) / per_block), unsigned(ns));
-        const unsigned lds = p->kind == ECGPU_KERNEL_PERM ? residency_lds_bytes(p->device) : 0u;
+        const unsigned lds = cap ? residency_lds_bytes(p->device) : 0u;
         ECGPU_HIP(launch(vec_fn, grid, block, a, stream, lds));
       }
       if (byte0 < p->size) {

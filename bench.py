@@ -171,6 +171,10 @@ def main():
     import erasure_coding_test_amd as E
     from erasure_coding_test_amd import _native as N
 
+    # ECGPU_BENCH_ONE_DEVICE=1: every rank on cuda:0 -- a multi-rank rehearsal
+    # on a one-GPU box (the numbers are then not a scaling measurement).
+    if os.environ.get("ECGPU_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     k, m, S, B = K_DATA, M_PARITY, SHARD, args.stripes

@@ -93,7 +93,26 @@ def load_traffic(workload: str):
     return None
 
 
-def cpu_baseline(seconds: float, threads: int = 1):
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_has_avx2() -> bool:
+    try:
+        with open("/proc/cpuinfo") as f:
+            return any(line.startswith("flags") and " avx2" in line for line in f)
+    except OSError:
+        return False
+
+
+def cpu_baseline(seconds: float, threads: int = 1, o3: bool = False):
     """Reference CPU path on the host: oracle/_ref (the reference's own
     src/erasure_coding compiled -O2) if shipped, else our C restatement.
     Bounded sample of the same workload: one RS(10,4) 4 MiB stripe, encode +
@@ -106,11 +125,14 @@ def cpu_baseline(seconds: float, threads: int = 1):
 
     import numpy as np
 
-    from oracle.oracle import Reference, Restatement, alloc_shards
-    try:
-        o = Reference()
-    except (FileNotFoundError, OSError):
-        o = Restatement()
+    from oracle.oracle import REFERENCE_O3_SO, Reference, Restatement, alloc_shards
+    if o3:
+        o = Reference(REFERENCE_O3_SO)  # caller checked avx2 and the file
+    else:
+        try:
+            o = Reference()
+        except (FileNotFoundError, OSError):
+            o = Restatement()
     k, m, S = K_DATA, M_PARITY, SHARD
     M = o.vandermonde_coding_matrix(k, m)
     rng = np.random.default_rng(0)
@@ -150,10 +172,12 @@ def cpu_baseline(seconds: float, threads: int = 1):
         if el >= seconds or iters >= 2000:
             break
     gib = iters * 2 * k * S / 2**30
-    src = "reference src/erasure_coding compiled g++ -O2" if o.kind == "reference" else "oracle/ec_oracle.c -O2"
+    flags = "-O3 -march=x86-64-v3" if o3 else "-O2"
+    src = f"reference src/erasure_coding compiled g++ {flags}" if o.kind == "reference" else "oracle/ec_oracle.c -O2"
     return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": threads, "kind": o.kind,
             "sample": f"{iters} x (RS(10,4) 4 MiB stripe encode + decode of erasure {{0}}), {threads} thread(s) "
-                      f"splitting byte ranges like client_main.cpp:1074-1164, {el:.1f} s, {src}"}
+                      f"splitting byte ranges like client_main.cpp:1074-1164, {el:.1f} s, {src}, "
+                      f"host CPU {cpu_model()}"}
 
 
 def host_threads() -> int:
@@ -236,10 +260,13 @@ def main():
 
     workload = f"RS(10,4) encode + decode{{0}}, 4 MiB shards, {B} stripes/GPU"
     if rank == 0:
-        cpu = cpu_all = None
+        cpu = cpu_all = cpu_o3 = None
         if world == 1 and args.cpu_seconds > 0:
             cpu = cpu_baseline(args.cpu_seconds)
             cpu_all = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_threads())
+            from oracle.oracle import REFERENCE_O3_SO
+            if host_has_avx2() and os.path.exists(REFERENCE_O3_SO):
+                cpu_o3 = cpu_baseline(max(2.0, args.cpu_seconds / 2), 1, o3=True)
         achieved = enc_bytes / (enc_ms / 1e3) / 1e9
         traffic = load_traffic(workload)
         out = {
@@ -267,6 +294,7 @@ def main():
                               "achieved_GBps": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1)},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
+            "cpu_baseline_o3": cpu_o3,
             "selfcheck_parity_ok": ok,
         }
         print(json.dumps(out), flush=True)

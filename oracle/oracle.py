@@ -29,6 +29,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 RESTATEMENT_SO = os.path.join(HERE, "libecoracle.so")
 REFERENCE_SO = os.path.join(HERE, "_ref", "libjerasure_ref.so")
+REFERENCE_O3_SO = os.path.join(HERE, "_ref", "libjerasure_ref_o3.so")  # -O3 -march=x86-64-v3
 
 _c_int_p = ctypes.POINTER(ctypes.c_int)
 _libc = ctypes.CDLL(None)

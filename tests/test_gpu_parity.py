@@ -689,3 +689,75 @@ def test_scheduled_operations_accumulate_many_rows(ec, gpu):
         want_b[(p + 1) % npk] ^= want_b[p]
     ec.jerasure.jerasure_do_scheduled_operations([a, b], ops, ps)
     assert np.array_equal(b.reshape(npk, ps), want_b)
+
+
+# ------------------------------------------------ structured data patterns ----
+def _pattern(name, size, shard):
+    i = np.arange(size, dtype=np.int64)
+    if name == "zeros":
+        return np.zeros(size, np.uint8)
+    if name == "ones":
+        return np.full(size, 0xFF, np.uint8)
+    if name == "ramp":
+        return ((i + shard) & 0xFF).astype(np.uint8)
+    return (1 << ((i + shard) % 8)).astype(np.uint8)  # single set bit per byte
+
+
+@pytest.mark.parametrize("name", ["zeros", "ones", "ramp", "single_bit"])
+@pytest.mark.parametrize("k,m", [(10, 4), (6, 3)])
+def test_structured_patterns_encode_decode(ec, gpu, restatement, name, k, m):
+    """SURVEY §8d correctness patterns (all-0x00, all-0xFF, ramp, single-bit)
+    through the device path, against the oracle restatement, then a decode of
+    m erased shards (data and parity mixed) back to the originals."""
+    import torch
+    size = (1 << 18) + 48
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = alloc_shards(k, size, PAD)
+    for j in range(k):
+        data[j][:size] = _pattern(name, size, j)
+    want = _encode_ref(restatement, k, m, M, data, size)
+    dd = to_dev(data, gpu)
+    dc = to_dev(alloc_shards(m, size, PAD), gpu)
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, dd, dc, size)
+    torch.cuda.synchronize()
+    got = to_host(dc)
+    for i in range(m):
+        assert np.array_equal(got[i][:size], want[i][:size]), i
+    er = [0, k - 1] + [k + i for i in range(m - 2)]
+    for e in er:
+        (dd + dc)[e].fill_(0x5C)
+    assert ec.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, er, dd, dc, size) == 0
+    torch.cuda.synchronize()
+    for j, t in enumerate(to_host(dd)):
+        assert np.array_equal(t[:size], data[j][:size]), j
+    for i, t in enumerate(to_host(dc)):
+        assert np.array_equal(t[:size], want[i][:size]), i
+
+
+@pytest.mark.parametrize("depth", [1, 4])
+def test_host_pipeline_depth_and_row_k_ones(ec, gpu, restatement, depth):
+    """Ring depth 1 (every submit waits for the previous stripe) and 4, and
+    the decoder's row_k_ones=1 shortcut (jerasure.cpp:232-239)."""
+    k, m, size, stripes = 6, 3, 65536 + 16, 5
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = [host_shards(42, s, k, size) for s in range(stripes)]
+    coding = [alloc_shards(m, size, PAD) for _ in range(stripes)]
+    p = ec.HostPipeline(k, m, M, size, depth=depth)
+    for s in range(stripes):
+        p.submit(data[s], coding[s])
+    p.drain()
+    p.close()
+    for s in range(stripes):
+        ref = _encode_ref(restatement, k, m, M, data[s], size)
+        for i in range(m):
+            assert np.array_equal(coding[s][i][:size], ref[i][:size]), (s, i)
+    saved = [d[3].copy() for d in data]
+    for d in data:
+        d[3][:] = 0
+    rd = ec.HostPipeline.decoder(k, m, M, [3], size, row_k_ones=1, depth=depth)
+    for s in range(stripes):
+        rd.submit(data[s], coding[s])
+    rd.drain()
+    rd.close()
+    for s in range(stripes):
+        assert np.array_equal(data[s][3][:size], saved[s][:size]), s

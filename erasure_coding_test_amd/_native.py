@@ -74,6 +74,13 @@ SIGNATURES = {
     "ecgpu_jerasure_do_scheduled_operations": (c_int, [c_void_pp, c_void_p, c_int]),
     "ecgpu_jerasure_schedule_encode": (c_int, [c_int, c_int, c_int, c_void_p, c_void_pp, c_void_pp, c_int, c_int]),
     "ecgpu_schedule_run": (c_int, [c_int, c_void_pp, c_void_p, c_int, c_int, c_int]),
+    "ecgpu_jerasure_dumb_bitmatrix_to_schedule": (c_void_p, [c_int, c_int, c_int, c_int_p]),
+    "ecgpu_jerasure_smart_bitmatrix_to_schedule": (c_void_p, [c_int, c_int, c_int, c_int_p]),
+    "ecgpu_jerasure_free_schedule": (None, [c_void_p]),
+    "ecgpu_jerasure_generate_schedule_cache": (c_void_p, [c_int, c_int, c_int, c_int_p, c_int]),
+    "ecgpu_jerasure_free_schedule_cache": (c_int, [c_int, c_int, c_void_p]),
+    "ecgpu_jerasure_schedule_decode_lazy": (c_int, [c_int, c_int, c_int, c_int_p, c_int_p, c_void_pp, c_void_pp, c_int, c_int, c_int]),
+    "ecgpu_jerasure_schedule_decode_cache": (c_int, [c_int, c_int, c_int, c_void_p, c_int_p, c_void_pp, c_void_pp, c_int, c_int]),
     "ecgpu_reed_sol_galois_w16_region_multby_2": (c_int, [c_void_p, c_int]),
     "ecgpu_reed_sol_galois_w32_region_multby_2": (c_int, [c_void_p, c_int]),
     "ecgpu_galois_w16_region_multiply": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int]),

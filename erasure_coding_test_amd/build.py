@@ -30,9 +30,9 @@ ARCH = os.environ.get("ECGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 
-HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "capi_host.cpp"]
+HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp"]
 HIP_SRCS = ["ecgpu_runtime.hip"]
-HDRS = ["gf_host.hpp", "matrix_host.hpp", "planner.hpp", "gf_kernels.hpp"]
+HDRS = ["gf_host.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp"]
 DROPIN_SRCS = ["jerasure_dropin.cpp", "jerasure_surface.cpp"]
 
 CXXFLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", f"-I{INCLUDE}", f"-I{CSRC}"]
@@ -83,7 +83,7 @@ def build_native(verbose: bool = True) -> dict:
                                      "-fvisibility-inlines-hidden", "-c", s, "-o", o])
         dropin_objs.append(o)
     # the CPU-surface code reuses the host GF / matrix objects (hidden symbols)
-    dropin_objs += [os.path.join(OBJ, s + ".o") for s in ("gf_host.cpp", "matrix_host.cpp")]
+    dropin_objs += [os.path.join(OBJ, s + ".o") for s in ("gf_host.cpp", "matrix_host.cpp", "schedule_host.cpp")]
     dropin = os.path.join(LIB, "libjerasure_amd.so")
     if _stale(dropin, dropin_objs + [ecgpu]):
         _run([CXX, "-shared", "-fPIC"] + dropin_objs +

@@ -7,6 +7,7 @@
 #include "gf_host.hpp"
 #include "matrix_host.hpp"
 #include "planner.hpp"
+#include "schedule_host.hpp"
 
 using namespace ecgpu;
 
@@ -66,6 +67,59 @@ ECGPU_API int ecgpu_jerasure_make_decoding_bitmatrix(int k, int m, int w, int* m
 }
 ECGPU_API int ecgpu_jerasure_invert_bitmatrix(int* mat, int* inv, int rows) { return invert_bitmatrix(mat, inv, rows); }
 ECGPU_API int ecgpu_jerasure_invertible_bitmatrix(int* mat, int rows) { return invertible_bitmatrix(mat, rows); }
+
+// ---------------------------------------------------------- schedules ----
+ECGPU_API int** ecgpu_jerasure_dumb_bitmatrix_to_schedule(int k, int m, int w, int* bitmatrix) {
+  return dumb_bitmatrix_to_schedule(k, m, w, bitmatrix);
+}
+ECGPU_API int** ecgpu_jerasure_smart_bitmatrix_to_schedule(int k, int m, int w, int* bitmatrix) {
+  return smart_bitmatrix_to_schedule(k, m, w, bitmatrix);
+}
+ECGPU_API void ecgpu_jerasure_free_schedule(int** schedule) { free_schedule(schedule); }
+ECGPU_API int*** ecgpu_jerasure_generate_schedule_cache(int k, int m, int w, int* bitmatrix, int smart) {
+  return generate_schedule_cache(k, m, w, bitmatrix, smart);
+}
+ECGPU_API int ecgpu_jerasure_free_schedule_cache(int k, int m, int*** cache) {
+  return free_schedule_cache(k, m, cache) == 0 ? ECGPU_OK : ECGPU_ERR_ARG;
+}
+
+// jerasure.cpp:935-961: schedule built on the host, executed on the GPU.
+ECGPU_API int ecgpu_jerasure_schedule_decode_lazy(int k, int m, int w, int* bitmatrix, int* erasures, char** data_ptrs,
+                                                  char** coding_ptrs, int size, int packetsize, int smart) {
+  if (k <= 0 || m <= 0 || w <= 0 || packetsize <= 0 || !bitmatrix || !erasures || size % (w * packetsize) != 0)
+    return ECGPU_ERR_ARG;
+  char** ptrs = schedule_ptrs(k, m, erasures, data_ptrs, coding_ptrs);
+  if (!ptrs) return ECGPU_ERR;
+  int** sched = decoding_schedule(k, m, w, bitmatrix, erasures, smart);
+  if (!sched) {
+    std::free(ptrs);
+    return ECGPU_ERR;
+  }
+  const int rc = ecgpu_schedule_run(k + m, ptrs, sched, w, size, packetsize);
+  free_schedule(sched);
+  std::free(ptrs);
+  return rc;
+}
+
+// jerasure.cpp:963-995: one or two erasures from a generate_schedule_cache table.
+ECGPU_API int ecgpu_jerasure_schedule_decode_cache(int k, int m, int w, int*** scache, int* erasures, char** data_ptrs,
+                                                   char** coding_ptrs, int size, int packetsize) {
+  if (k <= 0 || m <= 0 || w <= 0 || packetsize <= 0 || !scache || !erasures || size % (w * packetsize) != 0)
+    return ECGPU_ERR_ARG;
+  int index;
+  if (erasures[0] < 0) return ECGPU_ERR;
+  if (erasures[1] == -1)
+    index = erasures[0] * (k + m) + erasures[0];
+  else if (erasures[2] == -1)
+    index = erasures[0] * (k + m) + erasures[1];
+  else
+    return ECGPU_ERR;
+  char** ptrs = schedule_ptrs(k, m, erasures, data_ptrs, coding_ptrs);
+  if (!ptrs) return ECGPU_ERR;
+  const int rc = ecgpu_schedule_run(k + m, ptrs, scache[index], w, size, packetsize);
+  std::free(ptrs);
+  return rc;
+}
 
 // Replays the decode on symbolic buffers whose "pointers" are shard ids + 1,
 // then reads the fused map back in terms of ids.

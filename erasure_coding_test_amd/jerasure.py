@@ -192,13 +192,65 @@ def jerasure_schedule_encode(k: int, m: int, w: int, schedule, data_ptrs, coding
             "jerasure_schedule_encode")
 
 
+def _take_schedule(addr: int) -> List[Tuple[int, int, int, int, int]]:
+    """Copy a malloc'd int** schedule into tuples and free it."""
+    if not addr:
+        return None
+    rows = N.ctypes.cast(addr, N.ctypes.POINTER(N.ctypes.POINTER(N.c_int)))
+    ops, i = [], 0
+    while rows[i][0] >= 0:
+        ops.append(tuple(rows[i][j] for j in range(5)))
+        i += 1
+    N.lib.ecgpu_jerasure_free_schedule(addr)
+    return ops
+
+
 def jerasure_dumb_bitmatrix_to_schedule(k: int, m: int, w: int, bitmatrix) -> List[Tuple[int, int, int, int, int]]:
     """jerasure.cpp:1194-1224: one copy then XORs per output packet row."""
-    ops, cols = [], k * w
-    for r in range(m * w):
-        first = True
-        for c in range(cols):
-            if bitmatrix[r * cols + c]:
-                ops.append((c // w, c % w, k + r // w, r % w, 0 if first else 1))
-                first = False
-    return ops
+    return _take_schedule(N.lib.ecgpu_jerasure_dumb_bitmatrix_to_schedule(k, m, w, N.int_array(bitmatrix)))
+
+
+def jerasure_smart_bitmatrix_to_schedule(k: int, m: int, w: int, bitmatrix) -> List[Tuple[int, int, int, int, int]]:
+    """jerasure.cpp:1226-1344: rows built from an earlier row where cheaper."""
+    return _take_schedule(N.lib.ecgpu_jerasure_smart_bitmatrix_to_schedule(k, m, w, N.int_array(bitmatrix)))
+
+
+def jerasure_schedule_decode_lazy(k: int, m: int, w: int, bitmatrix, erasures, data_ptrs, coding_ptrs, size: int,
+                                  packetsize: int, smart: int) -> int:
+    """jerasure.cpp:935-961: decoding schedule built on the host, run on the MI355X."""
+    _check_packets("jerasure_schedule_decode_lazy", size, w, packetsize)
+    rc = N.lib.ecgpu_jerasure_schedule_decode_lazy(k, m, w, N.int_array(bitmatrix),
+                                                   N.int_array(_erasure_list(erasures)), N.ptr_array(addrs(data_ptrs)),
+                                                   N.ptr_array(addrs(coding_ptrs)), size, packetsize, smart)
+    return N.check(rc, "jerasure_schedule_decode_lazy")
+
+
+class ScheduleCache:
+    """jerasure_generate_schedule_cache (jerasure.cpp:997-1032; m must be 2):
+    decoding schedules for every one- and two-erasure pattern."""
+
+    def __init__(self, k: int, m: int, w: int, bitmatrix, smart: int = 1):
+        self.k, self.m, self.w = k, m, w
+        self._c = N.lib.ecgpu_jerasure_generate_schedule_cache(k, m, w, N.int_array(bitmatrix), smart)
+        if not self._c:
+            raise ValueError("jerasure_generate_schedule_cache: m must be 2")
+
+    def decode(self, erasures, data_ptrs, coding_ptrs, size: int, packetsize: int) -> int:
+        """jerasure_schedule_decode_cache (jerasure.cpp:963-995); -1 for more than two erasures."""
+        _check_packets("jerasure_schedule_decode_cache", size, self.w, packetsize)
+        rc = N.lib.ecgpu_jerasure_schedule_decode_cache(self.k, self.m, self.w, self._c,
+                                                        N.int_array(_erasure_list(erasures)),
+                                                        N.ptr_array(addrs(data_ptrs)), N.ptr_array(addrs(coding_ptrs)),
+                                                        size, packetsize)
+        return N.check(rc, "jerasure_schedule_decode_cache")
+
+    def close(self) -> None:
+        if getattr(self, "_c", None):
+            N.lib.ecgpu_jerasure_free_schedule_cache(self.k, self.m, self._c)
+            self._c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -131,6 +131,20 @@ ECGPU_API int ecgpu_jerasure_schedule_encode(int k, int m, int w, int** schedule
  * where unused): the engine behind schedule_encode and the scheduled decodes
  * (jerasure.cpp:935-995, whose schedules are built on the host). */
 ECGPU_API int ecgpu_schedule_run(int nptrs, char** ptrs, int** operations, int w, int size, int packetsize);
+/* Schedule construction (host) and scheduled decoding (host schedule, GPU
+ * execution): jerasure.cpp:1194-1224, :1226-1344, :534-541, :997-1032,
+ * :543-559 (returns ECGPU_ERR_ARG for m != 2 instead of exit), :935-961,
+ * :963-995.  Schedules are the reference's malloc'd int** (rows of 5,
+ * terminated by a row starting with -1). */
+ECGPU_API int** ecgpu_jerasure_dumb_bitmatrix_to_schedule(int k, int m, int w, int* bitmatrix);
+ECGPU_API int** ecgpu_jerasure_smart_bitmatrix_to_schedule(int k, int m, int w, int* bitmatrix);
+ECGPU_API void ecgpu_jerasure_free_schedule(int** schedule);
+ECGPU_API int*** ecgpu_jerasure_generate_schedule_cache(int k, int m, int w, int* bitmatrix, int smart);
+ECGPU_API int ecgpu_jerasure_free_schedule_cache(int k, int m, int*** cache);
+ECGPU_API int ecgpu_jerasure_schedule_decode_lazy(int k, int m, int w, int* bitmatrix, int* erasures, char** data_ptrs,
+                                                  char** coding_ptrs, int size, int packetsize, int smart);
+ECGPU_API int ecgpu_jerasure_schedule_decode_cache(int k, int m, int w, int*** scache, int* erasures, char** data_ptrs,
+                                                   char** coding_ptrs, int size, int packetsize);
 /* jerasure.cpp:1143-1151: fills xor, gf, memcpy byte counts and resets. */
 ECGPU_API int ecgpu_jerasure_get_stats(double* fill_in);
 

@@ -761,3 +761,34 @@ def test_host_pipeline_depth_and_row_k_ones(ec, gpu, restatement, depth):
     rd.close()
     for s in range(stripes):
         assert np.array_equal(data[s][3][:size], saved[s][:size]), s
+
+
+@pytest.mark.parametrize("smart", [0, 1])
+def test_schedule_decode_lazy_and_cache_device(ec, gpu, smart):
+    """Scheduled decoding through the Python mirror on device tensors: lazy
+    (any erasure set) and the m=2 schedule cache, against the originals."""
+    import torch
+    J = ec.jerasure
+    k, m, w, ps = 6, 2, 8, 512
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w)
+    bm = J.jerasure_matrix_to_bitmatrix(k, m, w, M)
+    size = w * ps * 5
+    rng = np.random.default_rng(7 + smart)
+    data = [torch.from_numpy(rng.integers(0, 256, size, dtype=np.uint8)).to(gpu) for _ in range(k)]
+    coding = [torch.zeros(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    J.jerasure_schedule_encode(k, m, w, J.jerasure_smart_bitmatrix_to_schedule(k, m, w, bm), data, coding, size, ps)
+    orig = [t.clone() for t in data + coding]
+    cache = J.ScheduleCache(k, m, w, bm, smart)
+    for er in ([0], [k], [1, 4], [2, k + 1], [k, k + 1]):
+        for method in ("lazy", "cache"):
+            for e in er:
+                (data + coding)[e].fill_(0xEE)
+            if method == "lazy":
+                assert J.jerasure_schedule_decode_lazy(k, m, w, bm, er, data, coding, size, ps, smart) == 0
+            else:
+                assert cache.decode(er, data, coding, size, ps) == 0
+            torch.cuda.synchronize()
+            for i, t in enumerate(data + coding):
+                assert torch.equal(t, orig[i]), (er, method, i)
+    assert cache.decode([0, 1, 2], data, coding, size, ps) == -1
+    cache.close()

@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--stripes", type=int, default=24, help="stripes per GPU per step (24 x 56 MiB = 1.3 GiB)")
+    ap.add_argument("--stripes", type=int, default=96,
+                    help="stripes per GPU per step (96 x 56 MiB = 5.3 GiB resident; throughput plateaus from 96, "
+                         "DESIGN.md §6)")
     ap.add_argument("--kernel", choices=["perm", "lds"], default="perm")
     ap.add_argument("--nt", type=int, default=1, help="non-temporal loads/stores")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")

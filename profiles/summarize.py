@@ -27,8 +27,8 @@ import statistics
 HERE = os.path.dirname(os.path.abspath(__file__))
 ENCODE = "gf_apply<10, 4, 3,"
 DECODE = "gf_apply<10, 1, 4,"
-WORKLOAD = "RS(10,4) encode + decode{0}, 4 MiB shards, 24 stripes/GPU"
-S, K, M, B = 4 << 20, 10, 4, 24
+WORKLOAD = "RS(10,4) encode + decode{0}, 4 MiB shards, 96 stripes/GPU"
+S, K, M, B = 4 << 20, 10, 4, 96
 
 
 def rows(path):

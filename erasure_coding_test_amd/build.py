@@ -31,8 +31,11 @@ HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 
 HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp"]
-HIP_SRCS = ["ecgpu_runtime.hip"]
-HDRS = ["gf_host.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp"]
+# (source, object, extra flags): the specialised kernel table is split into
+# one translation unit per output-row count so the four compile in parallel
+HIP_UNITS = [("ecgpu_runtime.hip", "ecgpu_runtime.hip.o", [])] + [
+    ("gf_spec.hip", f"gf_spec_r{r}.hip.o", [f"-DECGPU_SPEC_R={r}"]) for r in (1, 2, 3, 4)]
+HDRS = ["gf_host.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp", "gf_spec.hpp"]
 DROPIN_SRCS = ["jerasure_dropin.cpp", "jerasure_surface.cpp"]
 
 CXXFLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", f"-I{INCLUDE}", f"-I{CSRC}"]
@@ -43,6 +46,17 @@ HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE
 def _run(cmd):
     print("  " + " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+
+
+def _run_parallel(cmds):
+    """hipcc jobs in parallel (each is single-threaded); fails on the first error."""
+    from concurrent.futures import ThreadPoolExecutor
+    if not cmds:
+        return
+    workers = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 1), 8))
+    with ThreadPoolExecutor(workers) as ex:
+        for f in [ex.submit(_run, c) for c in cmds]:
+            f.result()
 
 
 def _stale(target, deps):
@@ -66,11 +80,13 @@ def build_native(verbose: bool = True) -> dict:
         if _stale(o, [s] + hdrs):
             _run([CXX] + CXXFLAGS + ["-fvisibility=hidden", "-c", s, "-o", o])
         objs.append(o)
-    for src in HIP_SRCS:
-        s, o = os.path.join(CSRC, src), os.path.join(OBJ, src + ".o")
+    jobs = []
+    for src, obj, extra in HIP_UNITS:
+        s, o = os.path.join(CSRC, src), os.path.join(OBJ, obj)
         if _stale(o, [s] + hdrs):
-            _run([HIPCC] + HIPFLAGS + ["-c", s, "-o", o])
+            jobs.append([HIPCC] + HIPFLAGS + extra + ["-c", s, "-o", o])
         objs.append(o)
+    _run_parallel(jobs)
     ecgpu = os.path.join(LIB, "libecgpu.so")
     if _stale(ecgpu, objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,-soname,libecgpu.so"] + objs + ["-o", ecgpu])

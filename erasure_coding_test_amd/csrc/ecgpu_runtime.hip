@@ -28,6 +28,7 @@
 #include "ecgpu.h"
 #include "gf_host.hpp"
 #include "gf_kernels.hpp"
+#include "gf_spec.hpp"
 #include "matrix_host.hpp"
 #include "planner.hpp"
 
@@ -59,42 +60,10 @@ int env_int(const char* name, int dflt) {
 // ------------------------------------------------------- kernel tables ----
 using KernelFn = void (*)(ApplyArgs);
 
-// Production kernel (A/B-chosen on MI355X): one 16-B column
-// per lane, v_perm multiply, XOR3 via v_bitop3, unit-coefficient structure
-// specialised at compile time (gf_kernels.hpp, UnitMask).
-template <int K, int R, int U>
-constexpr KernelFn apply_fn() { return &dev::gf_apply<K, R, U>; }
-template <int K, int R>
-constexpr KernelFn lds_fn() { return &dev::gf_apply_lds<K, R>; }
-
-constexpr int kUnitVariants[5] = {dev::kUnitNone, dev::kUnitCol0, dev::kUnitRow0, dev::kUnitCol0 | dev::kUnitRow0,
-                                  dev::kUnitAll};
-
-template <int K, int R>
-struct Cell {
-  static constexpr KernelFn apply[5] = {apply_fn<K, R, kUnitVariants[0]>(), apply_fn<K, R, kUnitVariants[1]>(),
-                                        apply_fn<K, R, kUnitVariants[2]>(), apply_fn<K, R, kUnitVariants[3]>(),
-                                        apply_fn<K, R, kUnitVariants[4]>()};
-};
-
-template <int K>
-struct Row {
-  static constexpr const KernelFn* apply[4] = {Cell<K, 1>::apply, Cell<K, 2>::apply, Cell<K, 3>::apply,
-                                               Cell<K, 4>::apply};
-  static constexpr KernelFn lds[4] = {lds_fn<K, 1>(), lds_fn<K, 2>(), lds_fn<K, 3>(), lds_fn<K, 4>()};
-};
-
-template <int... Ks>
-struct Table {
-  // unit_variant indexes kUnitVariants
-  static KernelFn get(bool lds, int K, int R, int unit_variant) {
-    KernelFn out = nullptr;
-    ((K == Ks ? (out = lds ? Row<Ks>::lds[R - 1] : Row<Ks>::apply[R - 1][unit_variant], 0) : 0), ...);
-    return out;
-  }
-};
-using SpecTable = Table<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>;
-
+// Production kernels: gf_apply<K, R, UNITS> specialised at compile time
+// (gf_spec.hpp, one translation unit per R): one 16-B column per lane,
+// 3-bit-slice v_perm multiply, XOR3 via v_bitop3, unit-coefficient
+// structure fixed per launch, non-temporal loads; store policy per launch.
 // Which compile-time unit structure holds exactly for rows [r0, r0+R).
 int unit_variant(const std::vector<uint32_t>& coef, int K, int r0, int R) {
   bool all = true, col0 = true, row0 = true;
@@ -126,15 +95,13 @@ hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t 
 // Residency cap for the streaming kernels.  Fewer resident workgroups per CU
 // means fewer DRAM pages open at once across the chip: with each lane reading
 // K shards and writing R, the uncapped kernel (VGPR-limited to 7 blocks/CU)
-// keeps ~28k distinct 4 KiB shard chunks in flight and loses to row-buffer
-// thrash.  3 blocks/CU measured (profiles/r01_residency_*.json):
-// RS(6,3) encode +21 %, RS(12,4) +6 %, RS(10,4) decode{0} +5 %, the bench
-// step +4.5 %; but a launch dense in GF multiplies (decode{0,1,2,3}: 40
-// non-unit coefficients over 14 shards) needs the occupancy to hide its VALU
-// work and loses 11 %, so launches with more than 2.5 multiply terms per
-// shard touched stay uncapped.  The cap is an unused dynamic LDS allocation
-// of LDS_per_CU / blocks (rounded down to 512 B).  ECGPU_BLOCKS_PER_CU
-// overrides the block count (0 = never cap).
+// keeps ~28k distinct 4 KiB shard chunks in flight.  3 blocks/CU measured
+// (DESIGN.md §5): decode{0} +9 %, RS(6,3) 1 MiB encode +6 %, RS(10,4) and
+// RS(12,4) encode neutral; a launch dense in GF multiplies (decode{0,1,2,3}:
+// 40 non-unit coefficients over 14 shards) needs the occupancy to hide its
+// VALU work and loses 7 %, so such launches stay uncapped (cap_for).  The
+// cap is an unused dynamic LDS allocation of LDS_per_CU / blocks (rounded
+// down to 512 B).  ECGPU_BLOCKS_PER_CU overrides the block count (0 = never).
 unsigned residency_lds_bytes(int device) {
   static std::once_flag once;
   static int per_cu = 0;
@@ -149,9 +116,25 @@ unsigned residency_lds_bytes(int device) {
   return b > unsigned(per_cu / (blocks + 1)) ? b : 0u;
 }
 
+// Per-launch policy of the production kernel (A/B on MI355X in the bench's
+// back-to-back context, DESIGN.md §5, profiles/r01_policy_ab.json):
+//   * stores non-temporal (loads always are): bench step +4 %, RS(10,4)
+//     encode 0.947 -> 0.889 ms, dense decode +9 %, RS(12,4) +6 %;
+//   * residency cap unless the launch is dense in GF multiplies (more than
+//     2.5 non-unit coefficients per shard touched): decode{0} +9 %, RS(6,3)
+//     +6 %; the 40-multiply decode{0,1,2,3} needs the occupancy (-7 % capped).
+// The store policy is the plan's `nt` flag (ECGPU_NT, ecgpu_plan_set_kernel;
+// default 1); ECGPU_CAP (0 = never, 1 = always) overrides the cap rule.
+bool cap_for(int K, int R, int mul_terms) {
+  static const int v = env_int("ECGPU_CAP", -1);
+  return v < 0 ? 2 * mul_terms <= 5 * (K + R) : (v != 0);
+}
+
 // Per-coefficient tables.  PERM: word p holds c*(e << 2p) in byte e.  LDS:
 // 16 low-nibble products then 16 high-nibble products.
-void build_tables(int c, u32x4* q, uint8_t* nib) {
+// P3 (production, gf_kernels.hpp mul3): T0[e] = c*e and T1[e] = c*(e << 3)
+// for e < 8 as dword pairs (low dword = entries 0..3), T2[e] = c*(e << 6).
+void build_tables(int c, u32x4* q, uint32_t* p3, uint8_t* nib) {
   const auto& T = gf8().mul[c & 0xFF];
   uint32_t w[4];
   for (int p = 0; p < 4; ++p) {
@@ -159,6 +142,12 @@ void build_tables(int c, u32x4* q, uint8_t* nib) {
     for (int e = 0; e < 4; ++e) w[p] |= uint32_t(T[e << (2 * p)]) << (8 * e);
   }
   *q = u32x4{w[0], w[1], w[2], w[3]};
+  for (int i = 0; i < dev::kP3Words; ++i) p3[i] = 0;
+  for (int e = 0; e < 8; ++e) {
+    p3[e >> 2] |= uint32_t(T[e]) << (8 * (e & 3));
+    p3[2 + (e >> 2)] |= uint32_t(T[e << 3]) << (8 * (e & 3));
+  }
+  for (int e = 0; e < 4; ++e) p3[4] |= uint32_t(T[e << 6]) << (8 * e);
   for (int x = 0; x < 16; ++x) {
     nib[x] = T[x];
     nib[16 + x] = T[x << 4];
@@ -206,6 +195,7 @@ struct ecgpu_plan {
   int kind = ECGPU_KERNEL_PERM, nt = 1;
   std::vector<uint32_t> coef;  // host copy, rows x nsrc
   u32x4* d_q = nullptr;
+  uint32_t* d_p3 = nullptr;   // 3-bit-slice tables, kP3Words per coefficient
   uint8_t* d_nib = nullptr;
   uint32_t* d_w = nullptr;     // wide-word tables (w = 16 / 32)
   uint8_t* d_wcls = nullptr;   // wide coefficient classes
@@ -235,6 +225,7 @@ void plan_free(ecgpu_plan* p) {
   if (!p) return;
   DeviceGuard g(p->device);
   if (p->d_q) (void)hipFree(p->d_q);
+  if (p->d_p3) (void)hipFree(p->d_p3);
   if (p->d_nib) (void)hipFree(p->d_nib);
   if (p->d_w) (void)hipFree(p->d_w);
   if (p->d_wcls) (void)hipFree(p->d_wcls);
@@ -271,12 +262,15 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
   }
   for (size_t i = 0; i < n; ++i) p->coef[i] = uint32_t(coefs[i]) & 0xFFu;
   std::vector<u32x4> q(n);
+  std::vector<uint32_t> p3(n * dev::kP3Words);
   std::vector<uint8_t> nib(n * 32);
-  for (size_t i = 0; i < n; ++i) build_tables(coefs[i], &q[i], &nib[i * 32]);
+  for (size_t i = 0; i < n; ++i) build_tables(coefs[i], &q[i], &p3[i * dev::kP3Words], &nib[i * 32]);
   DeviceGuard g(device);
   ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_q), n * sizeof(u32x4)));
+  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_p3), p3.size() * sizeof(uint32_t)));
   ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_nib), n * 32));
   ECGPU_HIP(hipMemcpy(p->d_q, q.data(), n * sizeof(u32x4), hipMemcpyHostToDevice));
+  ECGPU_HIP(hipMemcpy(p->d_p3, p3.data(), p3.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   ECGPU_HIP(hipMemcpy(p->d_nib, nib.data(), n * 32, hipMemcpyHostToDevice));
   return ECGPU_OK;
 }
@@ -373,13 +367,14 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
   for (int r0 = 0; r0 < p->rows; r0 += dev::kMaxRows) {
     const int R = std::min(dev::kMaxRows, p->rows - r0);
     const bool spec = K <= dev::kMaxSpecK;
-    KernelFn vec_fn = spec ? SpecTable::get(p->kind == ECGPU_KERNEL_LDS, K, R, unit_variant(p->coef, K, r0, R))
+    KernelFn vec_fn = spec ? spec_kernel(p->kind == ECGPU_KERNEL_LDS, K, R, unit_variant(p->coef, K, r0, R),
+                                         p->nt)
                            : generic_fn(R);
     const int vec = 1;
     int mul_terms = 0;  // coefficients that are neither 0 nor 1
     for (int r = 0; r < R; ++r)
       for (int j = 0; j < K; ++j) mul_terms += p->coef[size_t(r0 + r) * K + j] > 1u;
-    const bool cap = p->kind == ECGPU_KERNEL_PERM && 2 * mul_terms <= 5 * (K + R);
+    const bool cap = p->kind == ECGPU_KERNEL_PERM && cap_for(K, R, mul_terms);
     uint64_t unit = 0, zero = 0;
     if (spec)
       for (int r = 0; r < R; ++r)
@@ -392,6 +387,7 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
       const int ns = std::min(kMaxGridY, p->stripes - s0);
       ApplyArgs a{};
       a.qtab = p->d_q + size_t(r0) * K;
+      a.ptab = p->d_p3 + size_t(r0) * K * dev::kP3Words;
       a.ntab = p->d_nib + size_t(r0) * K * 32;
       a.src = p->d_src + size_t(s0) * K;
       a.dst = p->d_dst + size_t(s0) * p->rows;

@@ -39,6 +39,7 @@ constexpr uint32_t kLo2 = 0x03030303u;
 
 struct ApplyArgs {
   const u32x4* qtab;              // [R][K] PERM tables (16 B each)
+  const uint32_t* ptab;           // [R][K][kP3Words] 3-bit-slice PERM tables (production kernel)
   const uint8_t* ntab;            // [R][K][32] nibble tables (LDS engine)
   const uint8_t* const* src;      // [stripes][src_stride] device pointers
   uint8_t* const* dst;            // [stripes][dst_stride] device pointers
@@ -79,6 +80,24 @@ typedef __attribute__((address_space(1))) u32x4 gu32x4;
 __device__ __forceinline__ u32x4 load16(const uint8_t* p, int64_t col, int nt) {
   const gu32x4* a = (const gu32x4*)p + col;  // C cast: generic -> global address space
   return nt ? __builtin_nontemporal_load(a) : *a;
+}
+
+// Compile-time cache policy.  A runtime `nt ? nontemporal : plain` pair is
+// merged by the compiler into ONE plain access (the two loads differ only in
+// metadata), so the production kernels take the policy as a template
+// argument: NT = 1 emits the `nt` bit on the global_load / global_store.
+template <int NT>
+__device__ __forceinline__ u32x4 load16t(const uint8_t* p, int64_t col) {
+  const gu32x4* a = (const gu32x4*)p + col;
+  if constexpr (NT != 0) return __builtin_nontemporal_load(a);
+  else return *a;
+}
+
+template <int NT>
+__device__ __forceinline__ void store16t(uint8_t* p, int64_t col, const u32x4& v) {
+  gu32x4* a = (gu32x4*)p + col;
+  if constexpr (NT != 0) __builtin_nontemporal_store(v, a);
+  else *a = v;
 }
 
 __device__ __forceinline__ void store16(uint8_t* p, int64_t col, const u32x4& v, int nt) {
@@ -216,10 +235,113 @@ __device__ __forceinline__ uint32_t mac_word(uint32_t acc, const u32x4& q, uint3
   return xor3(acc, xor3(perm_lookup(q.x, s0), perm_lookup(q.y, s1), perm_lookup(q.z, s2)), perm_lookup(q.w, s3));
 }
 
+// 3-bit slices (production): v_perm picks from EIGHT bytes -- the pair
+// {hi, lo} -- so a byte splits into slices [0:2], [3:5], [6:7] and
+//   c*x = T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6],  Tp[e] = c*(e << 3p),
+// T0 and T1 each a dword pair, T2 one dword: 3 v_perm per coefficient-dword
+// instead of 4, and 5 selector ops per source dword instead of 7.  Table
+// layout per coefficient (kP3Words dwords): T0lo T0hi T1lo T1hi T2 (pad).
+constexpr int kP3Words = 8;
+constexpr uint32_t kLo3 = 0x07070707u;
+
+struct Sel3 {
+  uint32_t s0, s1, s2;
+};
+
+__device__ __forceinline__ Sel3 sel3(uint32_t x) { return Sel3{x & kLo3, (x >> 3) & kLo3, (x >> 6) & kLo2}; }
+
+// c*x for one dword, from the coefficient's table t and x's selectors.
+__device__ __forceinline__ uint32_t mul3(const uint32_t* __restrict__ t, const Sel3& s) {
+  return xor3(__builtin_amdgcn_perm(t[1], t[0], s.s0), __builtin_amdgcn_perm(t[3], t[2], s.s1),
+              __builtin_amdgcn_perm(t[4], t[4], s.s2));
+}
+
+// XOR accumulator that folds terms three at a time: v_bitop3 (XOR3) takes
+// the running value plus TWO new terms, so one odd term is parked until its
+// partner arrives.  N terms cost ceil(N/2) instead of N XORs (the compiler
+// does not reassociate the chain itself).  `has` is a compile-time constant
+// after full unrolling.
+struct Xacc {
+  uint32_t acc = 0u, pend = 0u;
+  bool has = false;
+  __device__ __forceinline__ void add(uint32_t v) {
+    if (has) {
+      acc = xor3(acc, pend, v);
+      has = false;
+    } else {
+      pend = v;
+      has = true;
+    }
+  }
+  __device__ __forceinline__ uint32_t value() const { return has ? (acc ^ pend) : acc; }
+};
+
+typedef __attribute__((address_space(4))) const uint32_t kconst_u32;
+
+__device__ __forceinline__ void mac3(Xacc& x, const kconst_u32* __restrict__ t, const Sel3& s) {
+  x.add(__builtin_amdgcn_perm(t[1], t[0], s.s0));
+  x.add(__builtin_amdgcn_perm(t[3], t[2], s.s1));
+  x.add(__builtin_amdgcn_perm(t[4], t[4], s.s2));
+}
+
+// R output columns from the K source columns of one lane, then R stores.
+// SLICES = 3: production 3-bit-slice tables (ptab); 2: the round-1 2-bit
+// form (qtab), kept for A/B timing in the diagnostic library.
+template <int K, int R, int UNITS, int SLICES, int NTS>
+__device__ __forceinline__ void combine_store(const ApplyArgs& a, const u32x4 (&x)[K], uint8_t* const (&dp)[R],
+                                              int64_t col) {
+  u32x4 acc[R];
+  if constexpr (SLICES == 3) {
+    Xacc xa[R][4];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      Sel3 sl[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sl[c] = sel3(x[j][c]);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (is_unit<UNITS>(r, j)) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) xa[r][c].add(x[j][c]);
+        } else {
+          // constant address space: always a scalar load, even after an
+          // LDS-DMA (which the compiler otherwise treats as a clobber)
+          const kconst_u32* t = (const kconst_u32*)a.ptab + (r * K + j) * kP3Words;  // C cast: generic -> constant
+#pragma unroll
+          for (int c = 0; c < 4; ++c) mac3(xa[r][c], t, sl[c]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = xa[r][c].value();
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (is_unit<UNITS>(r, j)) {
+          acc[r] ^= x[j];
+        } else {
+          const u32x4 q = a.qtab[r * K + j];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[r][c] = mac_word(acc[r][c], q, x[j][c]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) store16t<NTS>(dp[r], col, acc[r]);
+}
+
 // Lane l of block b handles the 16-byte columns (b*VEC + v)*256 + l, v < VEC,
 // of every shard of stripe s: all K*VEC loads are issued before any
-// arithmetic, then R*VEC stores.
-template <int K, int R, int UNITS, int VEC>
+// arithmetic, then R*VEC stores.  NT: bit 0 = non-temporal loads, bit 1 =
+// non-temporal stores (VEC == 1; the VEC > 1 probe form follows a.nt).
+template <int K, int R, int UNITS, int VEC, int SLICES = 3, int NT = 3>
 __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
   const unsigned cblk = a.stripe_fast ? blockIdx.y : blockIdx.x;
   const int s = a.stripe_fast ? blockIdx.x : blockIdx.y;
@@ -236,40 +358,10 @@ __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
   if constexpr (VEC == 1) {
     // Single column per lane (production): straight-line form, which keeps
     // the register allocation low (69 VGPRs for RS(10,4)).
-    const int64_t col = col0;
     u32x4 x[K];
-    if (a.nt) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, 1);
-    } else {
-#pragma unroll
-      for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, 0);
-    }
-    u32x4 acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (is_unit<UNITS>(r, j)) {
-          acc[r] ^= x[j];
-        } else {
-          const u32x4 q = a.qtab[r * K + j];
-          acc[r].x = mac_word(acc[r].x, q, x[j].x);
-          acc[r].y = mac_word(acc[r].y, q, x[j].y);
-          acc[r].z = mac_word(acc[r].z, q, x[j].z);
-          acc[r].w = mac_word(acc[r].w, q, x[j].w);
-        }
-      }
-    }
-    if (a.nt) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], 1);
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], 0);
-    }
+    for (int j = 0; j < K; ++j) x[j] = load16t<NT & 1>(sp[j], col0);
+    combine_store<K, R, UNITS, SLICES, (NT >> 1) & 1>(a, x, dp, col0);
     return;
   }
 
@@ -302,14 +394,12 @@ __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
 #pragma unroll
         for (int v = 0; v < VEC; ++v) acc[v][r] ^= x[v][j];
       } else {
-        const u32x4 q = a.qtab[r * K + j];
+        static_assert(SLICES == 3 || VEC == 1, "VEC > 1 uses the 3-bit-slice tables");
+        const uint32_t* t = a.ptab + (r * K + j) * kP3Words;
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          acc[v][r].x = mac_word(acc[v][r].x, q, x[v][j].x);
-          acc[v][r].y = mac_word(acc[v][r].y, q, x[v][j].y);
-          acc[v][r].z = mac_word(acc[v][r].z, q, x[v][j].z);
-          acc[v][r].w = mac_word(acc[v][r].w, q, x[v][j].w);
-        }
+        for (int v = 0; v < VEC; ++v)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[v][r][c] ^= mul3(t, sel3(x[v][j][c]));
       }
     }
   }
@@ -327,9 +417,45 @@ __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
   }
 }
 
-template <int K, int R, int UNITS, int VEC = 1>
+// Production cache policy (A/B on MI355X): non-temporal loads
+// and stores (NT = 3).  The runtime can select plain stores per launch
+// (gf_spec.hpp store_nt) for tuning.
+template <int K, int R, int UNITS, int VEC = 1, int SLICES = 3, int NT = 3>
 __global__ __launch_bounds__(kBlock) void gf_apply(ApplyArgs a) {
-  gf_apply_body<K, R, UNITS, VEC>(a);
+  gf_apply_body<K, R, UNITS, VEC, SLICES, NT>(a);
+}
+
+// LDS-DMA form: the K source columns of a lane arrive by
+// global_load_lds_dwordx4 (one 1 KiB piece per wave-instruction, written to
+// LDS at wave base + lane*16, no VGPR destination) instead of register
+// loads; the lane reads back only its own 16 B, so no barrier is needed,
+// just the wait on the VM counter.  K KiB of LDS per wave.
+template <int K, int R, int UNITS, int SLICES = 3, int NT = 3>
+__global__ __launch_bounds__(kBlock) void gf_apply_dma(ApplyArgs a) {
+  __shared__ __attribute__((aligned(16))) u32x4 stage[kBlock / 64][K][64];
+  const int s = blockIdx.y;
+  const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  // all pointers first (scalar loads), then the DMA issue
+  const uint8_t* src[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) src[j] = sp[j];
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + col * 16),
+                                     (__attribute__((address_space(3))) void*)&stage[w][j][0], 16, 0,
+                                     (NT & 1) ? 2 : 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = stage[w][j][lane];
+  combine_store<K, R, UNITS, SLICES, (NT >> 1) & 1>(a, x, dp, col);
 }
 
 // Same body, register budget capped for 8 waves/SIMD (<= 64 VGPRs).
@@ -409,7 +535,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm_stream(ApplyArgs a) {
 }
 
 // DIAGNOSTIC: streaming copy of shard 0 -> dst 0 (the HBM ceiling reference).
-template <int VEC>
+// NT: bit 0 = non-temporal loads, bit 1 = non-temporal stores.
+template <int VEC, int NT = 1>
 __global__ __launch_bounds__(kBlock) void diag_copy(ApplyArgs a) {
   const int64_t col0 = int64_t(blockIdx.x) * (VEC * kBlock) + threadIdx.x;
   const int s = blockIdx.y;
@@ -418,10 +545,10 @@ __global__ __launch_bounds__(kBlock) void diag_copy(ApplyArgs a) {
   u32x4 x[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v)
-    if (col0 + v * kBlock < a.nvec) x[v] = load16(sp, col0 + v * kBlock, a.nt);
+    if (col0 + v * kBlock < a.nvec) x[v] = load16t<NT & 1>(sp, col0 + v * kBlock);
 #pragma unroll
   for (int v = 0; v < VEC; ++v)
-    if (col0 + v * kBlock < a.nvec) store16(dp, col0 + v * kBlock, x[v], a.nt);
+    if (col0 + v * kBlock < a.nvec) store16t<(NT >> 1) & 1>(dp, col0 + v * kBlock, x[v]);
 }
 
 // ----------------------------------------------------------------- LDS ----
@@ -453,7 +580,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
 
   u32x4 x[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) x[j] = load16(sp[j], col, a.nt);
+  for (int j = 0; j < K; ++j) x[j] = load16t<1>(sp[j], col);
 
   u32x4 acc[R];
 #pragma unroll
@@ -500,7 +627,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm_generic(ApplyArgs a) {
   for (; j + 4 <= K; j += 4) {
     u32x4 x[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = load16(sp[j + u], col, a.nt);
+    for (int u = 0; u < 4; ++u) x[u] = load16t<1>(sp[j + u], col);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const u32x4 v = x[u];
@@ -521,7 +648,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm_generic(ApplyArgs a) {
     }
   }
   for (; j < K; ++j) {
-    const u32x4 v = load16(sp[j], col, a.nt);
+    const u32x4 v = load16t<1>(sp[j], col);
     const u32x4 s0 = v & kLo2, s1 = (v >> 2) & kLo2, s2 = (v >> 4) & kLo2, s3 = (v >> 6) & kLo2;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -538,7 +665,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm_generic(ApplyArgs a) {
 
 // --------------------------------------- bytes: tails, misaligned shards ----
 // One lane per byte in [byte0, size); any K, R <= kMaxRows, any alignment.
-__global__ __launch_bounds__(kBlock) void gf_apply_bytes(ApplyArgs a) {
+static __global__ __launch_bounds__(kBlock) void gf_apply_bytes(ApplyArgs a) {
   const int64_t x = a.byte0 + int64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (x >= a.size) return;
   const int s = blockIdx.y;
@@ -629,7 +756,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide(ApplyArgs a) {
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
   for (int j = 0; j < a.K; ++j) {
-    const u32x4 x = load16(sp[j], col, a.nt);
+    const u32x4 x = load16t<1>(sp[j], col);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       uint32_t sel[Wide<W>::kPerms];
@@ -755,7 +882,7 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets(PacketArgs a) {
 }
 
 // Byte form for packet sizes / bases that are not 8-byte aligned.
-__global__ __launch_bounds__(kBlock) void gf_xor_packets_bytes(PacketArgs a) {
+static __global__ __launch_bounds__(kBlock) void gf_xor_packets_bytes(PacketArgs a) {
   const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (g >= a.ncols) return;
   int64_t sp, col;

@@ -1,0 +1,32 @@
+// gf_spec.hpp -- the compile-time-specialised production kernels
+// (gf_kernels.hpp gf_apply<K, R, UNITS, 1, 3, NT> and gf_apply_lds<K, R>)
+// for K = 1..kMaxSpecK sources.  Instantiated in four translation units, one
+// per output-row count R (gf_spec.hip built with -DECGPU_SPEC_R=1..4), so
+// the build compiles them in parallel.
+#pragma once
+#include "gf_kernels.hpp"
+
+namespace ecgpu {
+
+using SpecKernelFn = void (*)(dev::ApplyArgs);
+
+// Store cache policy of the production kernel: 0 plain, 1 non-temporal.
+// (Loads are always non-temporal.)  kind: ECGPU_KERNEL_PERM / _LDS.
+// unit_variant indexes kUnitVariants (ecgpu_runtime.hip).  nullptr if K is
+// outside 1..kMaxSpecK.
+SpecKernelFn spec_kernel_r1(bool lds, int K, int unit_variant, int store_nt);
+SpecKernelFn spec_kernel_r2(bool lds, int K, int unit_variant, int store_nt);
+SpecKernelFn spec_kernel_r3(bool lds, int K, int unit_variant, int store_nt);
+SpecKernelFn spec_kernel_r4(bool lds, int K, int unit_variant, int store_nt);
+
+inline SpecKernelFn spec_kernel(bool lds, int K, int R, int unit_variant, int store_nt) {
+  switch (R) {
+    case 1: return spec_kernel_r1(lds, K, unit_variant, store_nt);
+    case 2: return spec_kernel_r2(lds, K, unit_variant, store_nt);
+    case 3: return spec_kernel_r3(lds, K, unit_variant, store_nt);
+    case 4: return spec_kernel_r4(lds, K, unit_variant, store_nt);
+    default: return nullptr;
+  }
+}
+
+}  // namespace ecgpu

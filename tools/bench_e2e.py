@@ -225,13 +225,17 @@ def device_configs():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stripes", type=int, default=48)
+    ap.add_argument("--parts", default="", help="comma list of result keys to run (default: all)")
     a = ap.parse_args()
-    res = {"pcie": pcie_rates(), "e2e_pinned": e2e_pinned(a.stripes),
-           "e2e_pipeline_pinned": e2e_pipeline(a.stripes), "e2e_pipeline_pageable": e2e_pipeline(a.stripes, pinned=False),
-           "e2e_read_pipeline_1": e2e_read_pipeline([0], a.stripes),
-           "e2e_read_pipeline_4": e2e_read_pipeline([0, 1, 2, 3], a.stripes),
-           "dropin_pageable": dropin_pageable(),
-           "device_configs": device_configs()}
+    parts = {"pcie": pcie_rates, "e2e_pinned": lambda: e2e_pinned(a.stripes),
+             "e2e_pipeline_pinned": lambda: e2e_pipeline(a.stripes),
+             "e2e_pipeline_pageable": lambda: e2e_pipeline(a.stripes, pinned=False),
+             "e2e_read_pipeline_1": lambda: e2e_read_pipeline([0], a.stripes),
+             "e2e_read_pipeline_4": lambda: e2e_read_pipeline([0, 1, 2, 3], a.stripes),
+             "dropin_pageable": dropin_pageable,
+             "device_configs": device_configs}
+    want = a.parts.split(",") if a.parts else list(parts)
+    res = {name: parts[name]() for name in want}
     print(json.dumps(res, indent=1))
 
 

@@ -26,18 +26,27 @@ from erasure_coding_test_amd import _native as N  # noqa: E402
 L = ctypes.CDLL(os.path.join(N.LIB_DIR, "libecgpu_diag.so"))
 L.ecgpu_diag_launch.restype = ctypes.c_int
 L.ecgpu_diag_launch.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p] * 4 + [
-    ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_void_p]
+    ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_void_p,
+    ctypes.c_void_p]
+P3 = {}  # id(qtab tensor) -> 3-bit-slice tables of the same coefficients
 
 
 def tables(coefs):
     gm = E.galois.galois_single_multiply
-    q, nib = [], []
+    q, nib, p3 = [], [], []
     for c in coefs:
         for p in range(4):
             q.append(sum(gm(c, e << (2 * p), 8) << (8 * e) for e in range(4)))
         nib += [gm(c, x, 8) for x in range(16)] + [gm(c, x << 4, 8) for x in range(16)]
-    return (torch.tensor(q, dtype=torch.int64).to(torch.int32).cuda(),
-            torch.tensor(nib, dtype=torch.uint8).cuda())
+        # P3 layout (ecgpu_runtime.hip build_tables): T0lo T0hi T1lo T1hi T2 pad pad pad
+        w = lambda vals: sum(v << (8 * e) for e, v in enumerate(vals))
+        t0 = [gm(c, e, 8) for e in range(8)]
+        t1 = [gm(c, e << 3, 8) for e in range(8)]
+        t2 = [gm(c, e << 6, 8) for e in range(4)]
+        p3 += [w(t0[:4]), w(t0[4:]), w(t1[:4]), w(t1[4:]), w(t2), 0, 0, 0]
+    qt = torch.tensor(q, dtype=torch.int64).to(torch.int32).cuda()
+    P3[id(qt)] = torch.tensor(p3, dtype=torch.int64).to(torch.int32).cuda()
+    return qt, torch.tensor(nib, dtype=torch.uint8).cuda()
 
 
 def masks(coefs):
@@ -92,9 +101,10 @@ def run_layout(args, k, m, S, B, pad):
     stream = torch.cuda.current_stream().cuda_stream
 
     variants = []
+    for ntb in range(4):  # copy reference: cache policy bits (loads / stores)
+        variants.append((f"copy vec1 ldnt{ntb & 1} stnt{ntb >> 1}", 1, 1, 1, 1, ntb, None, None, src_cp, dst_cp,
+                         7 * B, 0, 0, 2 * S * 7 * B, 1))
     for nt in (1, 0):
-        variants.append((f"copy vec1 nt{nt}", 1, 1, 1, 1, 0, None, None, src_cp, dst_cp, 7 * B, 0, 0,
-                         2 * S * 7 * B, nt))
         for vec in (1, 2):
             for mode, mname in ((2, "allperm"), (3, "xoronly")):
                 variants.append((f"enc perm vec{vec} {mname} nt{nt}", 0, 10, 4, vec, mode, q_enc, n_enc, src_enc,
@@ -111,6 +121,9 @@ def run_layout(args, k, m, S, B, pad):
                          z_enc, (k + m) * S * B, nt))
         variants.append((f"enc apply rs stripefast nt{nt}", 5, 10, 4, 1, 3, q_enc, n_enc, src_enc, dst_enc, B, u_enc,
                          z_enc, (k + m) * S * B, nt))
+    # production body with the round-1 2-bit-slice tables (A/B vs "enc apply rs nt1")
+    variants.append(("enc apply2 rs nt1", 10, 10, 4, 1, 3, q_enc, n_enc, src_enc, dst_enc, B, u_enc, z_enc,
+                     (k + m) * S * B, 1))
     variants.append(("enc lds nt1", 2, 10, 4, 1, 0, q_enc, n_enc, src_enc, dst_enc, B, u_enc, z_enc,
                      (k + m) * S * B, 1))
     for name, row in dec_rows.items():
@@ -121,6 +134,8 @@ def run_layout(args, k, m, S, B, pad):
         for var, tag in ((4, ""), (5, " stripefast"), (6, " occ8")):
             variants.append((f"dec1 {name} apply {'all' if name == 'ones' else 'none'}{tag} nt1", var, 10, 1, 1,
                              4 if name == "ones" else 0, qd, nd, src_dec, dst_dec, B, ud, zd, (k + 1) * S * B, 1))
+        variants.append((f"dec1 {name} apply2 nt1", 10, 10, 1, 1, 4 if name == "ones" else 0, qd, nd, src_dec,
+                         dst_dec, B, ud, zd, (k + 1) * S * B, 1))
         for bps in (32, 64):
             variants.append((f"dec1 {name} stream bps{bps} nt1", 3, 10, 1, bps, 2, qd, nd, src_dec, dst_dec, B, ud,
                              zd, (k + 1) * S * B, 1))
@@ -146,6 +161,44 @@ def run_layout(args, k, m, S, B, pad):
         st = ptr_table([addr(s, j) for s in range(B) for j in range(K2)])
         dt = ptr_table([addr(s, K2 + i) for s in range(B) for i in range(R2)])
         variants.append((f"P xor K{K2} R{R2}", 9, K2, R2, 1, 3, q_enc, n_enc, st, dt, B, 0, 0, (K2 + R2) * S * B, 1))
+    # read-only probes: K streams read, nothing written (diag variants 11 / 12)
+    for K2 in (1, 4, 10, 14):
+        st = ptr_table([addr(s, j) for s in range(B) for j in range(K2)])
+        dt = ptr_table([addr(s, 0) for s in range(B)])
+        variants.append((f"R regs K{K2}", 11, K2, 1, 1, 0, q_enc, n_enc, st, dt, B, 0, 0, K2 * S * B, 1))
+        for nt in (1, 0):
+            variants.append((f"R glds K{K2} nt{nt}", 12, K2, 1, 1, 0, q_enc, n_enc, st, dt, B, 0, 0, K2 * S * B, nt))
+    # cache-policy / load-path factorial of the production combine (diag 13 / 14)
+    qd1, nd1 = tables(dec_rows["ones"])
+    ud1, zd1 = masks(dec_rows["ones"])
+    for var, path in ((13, "regs"), (14, "dma")):
+        for ntb in range(4):
+            tag = f"ldnt{ntb & 1} stnt{ntb >> 1}"
+            variants.append((f"X enc {path} {tag}", var, 10, 4, ntb, 3, q_enc, n_enc, src_enc, dst_enc, B, u_enc,
+                             z_enc, (k + m) * S * B, 1))
+            variants.append((f"X dec1 {path} {tag}", var, 10, 1, ntb, 4, qd1, nd1, src_dec, dst_dec, B, ud1, zd1,
+                             (k + 1) * S * B, 1))
+    # other launch shapes of the BASELINE configs, same factorial (register loads)
+    M63 = E.reed_sol.reed_sol_vandermonde_coding_matrix(6, 3, 8)
+    q63, n63 = tables(M63)
+    u63, z63 = masks(M63)
+    src63 = ptr_table([addr(s, j) for s in range(B) for j in range(6)])
+    dst63 = ptr_table([addr(s, 6 + i) for s in range(B) for i in range(3)])
+    dense4 = [150, 119, 240, 20, 249, 36, 126, 92, 191, 156, 234, 203, 20, 62, 66, 253, 51, 81, 244, 150,
+              105, 20, 32, 68, 153, 129, 237, 70, 41, 130, 20, 169, 197, 111, 35, 89, 161, 75, 98, 136]
+    q4d, n4d = tables(dense4)
+    u4d, z4d = masks(dense4)
+    src4d = ptr_table([addr(s, j) for s in range(B) for j in range(4, 14)])
+    dst4d = ptr_table([addr(s, i) for s in range(B) for i in range(4)])
+    qdd, ndd = tables(dec_rows["dense"])
+    udd, zdd = masks(dec_rows["dense"])
+    for ntb in range(4):
+        tag = f"ldnt{ntb & 1} stnt{ntb >> 1}"
+        variants.append((f"Y enc63 {tag}", 13, 6, 3, ntb, 3, q63, n63, src63, dst63, B, u63, z63, 9 * S * B, 1))
+        variants.append((f"Y dec4dense {tag}", 13, 10, 4, ntb, 0, q4d, n4d, src4d, dst4d, B, u4d, z4d,
+                         14 * S * B, 1))
+        variants.append((f"Y dec1dense {tag}", 13, 10, 1, ntb, 0, qdd, ndd, src_dec, dst_dec, B, udd, zdd,
+                         11 * S * B, 1))
     variants = [v for v in variants if any(o in v[0] for o in only)]
     times = {v[0]: [] for v in variants}
     import random
@@ -161,7 +214,8 @@ def run_layout(args, k, m, S, B, pad):
                 e0.record()
                 rc = L.ecgpu_diag_launch(var, K, R, vec, mode, qt.data_ptr() if qt is not None else None,
                                          nb.data_ptr() if nb is not None else None, st.data_ptr(), dt.data_ptr(),
-                                         stripes, S, um, zm, nt, stream)
+                                         stripes, S, um, zm, nt, stream,
+                                         P3[id(qt)].data_ptr() if qt is not None else None)
                 e1.record()
                 assert rc == 0, (name, rc)
                 torch.cuda.synchronize()

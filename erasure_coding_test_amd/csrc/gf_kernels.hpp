@@ -606,7 +606,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
     }
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], a.nt);
+  for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
 }
 
 // ------------------------------------------- generic K (> kMaxSpecK) ----
@@ -660,7 +660,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm_generic(ApplyArgs a) {
     }
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], a.nt);
+  for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
 }
 
 // --------------------------------------- bytes: tails, misaligned shards ----
@@ -730,8 +730,8 @@ __device__ __forceinline__ void wide_sel(uint32_t x, uint32_t (&sel)[Wide<W>::kP
   }
 }
 
-template <int W>
-__device__ __forceinline__ uint32_t wide_mac(uint32_t acc, const uint32_t* __restrict__ t,
+template <int W, typename TP>
+__device__ __forceinline__ uint32_t wide_mac(uint32_t acc, const TP* __restrict__ t,
                                              const uint32_t (&sel)[Wide<W>::kPerms]) {
 #pragma unroll
   for (int i = 0; i < Wide<W>::kPerms; i += 2)
@@ -752,29 +752,51 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide(ApplyArgs a) {
 #pragma unroll
   for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
   constexpr int kWords = 2 * Wide<W>::kPerms;
+  // sources in chunks of kWideChunk: every load of a chunk is in flight
+  // before its first use (a load-use loop over runtime K keeps one 16-B load
+  // per lane in flight and is latency-bound)
+  constexpr int kWideChunk = 8;
   u32x4 acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
-  for (int j = 0; j < a.K; ++j) {
-    const u32x4 x = load16t<1>(sp[j], col);
+  for (int j0 = 0; j0 < a.K; j0 += kWideChunk) {
+    u32x4 xs[kWideChunk];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      uint32_t sel[Wide<W>::kPerms];
-      wide_sel<W>(x[c], sel);
+    for (int u = 0; u < kWideChunk; ++u)
+      if (j0 + u < a.K) xs[u] = load16t<1>(sp[j0 + u], col);
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint8_t cls = a.wcls[r * a.K + j];
-        if (cls == 2) continue;
-        if (cls == 1) {
-          acc[r][c] ^= x[c];
-          continue;
+    for (int u = 0; u < kWideChunk; ++u) {
+      const int j = j0 + u;
+      if (j >= a.K) break;
+      const u32x4 x = xs[u];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t sel[Wide<W>::kPerms];
+        wide_sel<W>(x[c], sel);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if constexpr (W == 2) {
+            // branch-free at w = 16: a unit or zero coefficient's tables are
+            // the identity / zero map, so every term goes through wide_mac and
+            // the chunk body is straight-line (352 vs 410 us per 64 MiB
+            // RS(10,4) encode).  At w = 32 (32 v_perm per term) skipping the
+            // 13 unit terms wins instead (1.18 vs 2.72 ms).
+            acc[r][c] = wide_mac<W>(acc[r][c], (const kconst_u32*)a.wtab + size_t(r * a.K + j) * kWords, sel);
+          } else {
+            const uint8_t cls = a.wcls[r * a.K + j];
+            if (cls == 2) continue;
+            if (cls == 1) {
+              acc[r][c] ^= x[c];
+              continue;
+            }
+            acc[r][c] = wide_mac<W>(acc[r][c], a.wtab + size_t(r * a.K + j) * kWords, sel);
+          }
         }
-        acc[r][c] = wide_mac<W>(acc[r][c], a.wtab + size_t(r * a.K + j) * kWords, sel);
       }
     }
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) store16(dp[r], col, acc[r], a.nt);
+  for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
 }
 
 // Words from byte0 to size (tails, or whole regions whose pointers are not
@@ -843,6 +865,9 @@ __device__ __forceinline__ void packet_coords(const PacketArgs& a, int64_t g, in
 
 template <int RT>
 __device__ __forceinline__ void xor_masked(uint32_t (&acc)[RT][2], const u32x2& x, uint32_t m) {
+  // Row selectors as wave-uniform SALU values.  (Extracting them in VGPRs
+  // with v_bfe_i32 avoids the compiler's SGPR spills to VGPR lanes but was
+  // slower: 269 vs 240 us per 64 MiB RS(10,4) bit-matrix encode.)
 #pragma unroll
   for (int r = 0; r < RT; ++r) {
     const uint32_t sel = uint32_t(int32_t(m << (31 - r)) >> 31);  // 0 or ~0, wave-uniform (SALU)

@@ -191,6 +191,50 @@ def dropin_pageable(k=10, m=4, S=4 << 20, reps=5):
             "decode_ms": round(td * 1e3, 2), "decode_ok": bool(np.array_equal(bufs[0], saved))}
 
 
+def ecx_accum(k=10, m=4, S=4 << 20, stripes=12):
+    """ECX incremental accumulation (ecx_datanode_main.cpp:680-735) through
+    ParityAccumulator: per stripe, k synchronous adds (one arriving source
+    block each, coefficient column j of the coding matrix) into m HBM-resident
+    accumulators, then m reads of the finished parity.  Blocks device-resident,
+    in pinned host memory, or in pageable host memory; the parity read goes to
+    the same kind of memory.  HBM bytes per stripe: k blocks read, m
+    accumulators written once and read+written k-1 times."""
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    cols = [[M[i * k + j] for i in range(m)] for j in range(k)]
+    out = {}
+    for where in ("device", "pinned", "pageable"):
+        if where == "device":
+            blocks = torch.randint(0, 256, (k, S), dtype=torch.uint8, device="cuda")
+            parity = torch.empty((m, S), dtype=torch.uint8, device="cuda")
+        else:
+            blocks = torch.randint(0, 256, (k, S), dtype=torch.uint8)
+            parity = torch.empty((m, S), dtype=torch.uint8)
+            if where == "pinned":
+                blocks, parity = blocks.pin_memory(), parity.pin_memory()
+        acc = E.ParityAccumulator(m, S)
+
+        def one():
+            acc.reset()
+            for j in range(k):
+                acc.add(blocks[j], cols[j])
+            for i in range(m):
+                acc.read(i, parity[i])
+
+        one()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(stripes):
+            one()
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / stripes
+        hbm = (k + m + 2 * m * (k - 1)) * S
+        out[where] = {"stripe_ms": round(t * 1e3, 3), "per_add_us": round(t / k * 1e6, 1),
+                      "data_GiBps": round(k * S / t / GiB, 2), "hbm_GBps_if_device": round(hbm / t / 1e9, 1)}
+        acc.close()
+    return {"workload": f"ParityAccumulator RS({k},{m}), {S >> 20} MiB blocks, {k} adds + {m} reads per stripe, "
+                        f"{stripes} stripes, synchronous calls", "results": out}
+
+
 def device_configs():
     out = []
     cases = [("C2 RS(6,3) 1 MiB encode", 6, 3, 1 << 20, 96, None),
@@ -233,6 +277,7 @@ def main():
              "e2e_read_pipeline_1": lambda: e2e_read_pipeline([0], a.stripes),
              "e2e_read_pipeline_4": lambda: e2e_read_pipeline([0, 1, 2, 3], a.stripes),
              "dropin_pageable": dropin_pageable,
+             "ecx_accum": ecx_accum,
              "device_configs": device_configs}
     want = a.parts.split(",") if a.parts else list(parts)
     res = {name: parts[name]() for name in want}

@@ -275,8 +275,11 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
   return ECGPU_OK;
 }
 
+// With a stream the pointer tables are uploaded asynchronously on it; unless
+// `keep_alive` (the caller keeps src/dst alive until it synchronises the
+// stream, as execute() does) the call waits for the upload.
 int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* const* dst, int64_t size,
-              hipStream_t stream) {
+              hipStream_t stream, bool keep_alive = false) {
   const size_t ns = size_t(stripes) * p->nsrc, nd = size_t(stripes) * p->rows;
   DeviceGuard g(p->device);
   if (ns > p->cap_src) {
@@ -297,7 +300,7 @@ int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* co
   if (stream) {
     ECGPU_HIP(hipMemcpyAsync(p->d_src, src, ns * sizeof(void*), hipMemcpyHostToDevice, stream));
     ECGPU_HIP(hipMemcpyAsync(p->d_dst, dst, nd * sizeof(void*), hipMemcpyHostToDevice, stream));
-    ECGPU_HIP(hipStreamSynchronize(stream));  // host tables may die after return
+    if (!keep_alive) ECGPU_HIP(hipStreamSynchronize(stream));  // host tables may die after return
   } else {
     ECGPU_HIP(hipMemcpy(p->d_src, src, ns * sizeof(void*), hipMemcpyHostToDevice));
     ECGPU_HIP(hipMemcpy(p->d_dst, dst, nd * sizeof(void*), hipMemcpyHostToDevice));
@@ -608,7 +611,7 @@ int execute(const FusedOp& op, int64_t size) {
     ecgpu_plan* p = nullptr;
     rc = ctx_plan(c, rows, nsrc, op.coef, op.w, &p);
     if (rc != ECGPU_OK) return rc;
-    rc = plan_bind(p, 1, sp.data(), dp.data(), size, c->stream);
+    rc = plan_bind(p, 1, sp.data(), dp.data(), size, c->stream, /*keep_alive=*/true);  // sp/dp outlive the sync below
     if (rc != ECGPU_OK) return rc;
     rc = plan_launch(p, c->stream);
     if (rc != ECGPU_OK) return rc;

@@ -235,6 +235,35 @@ def ecx_accum(k=10, m=4, S=4 << 20, stripes=12):
                         f"{stripes} stripes, synchronous calls", "results": out}
 
 
+def call_latency(reps=200):
+    """Fixed cost of one synchronous drop-in call (host planning, pointer
+    classification, pointer-table upload, launch, stream sync): RS(10,4)
+    jerasure_matrix_encode / decode{0} on 4 KiB device-resident shards, and
+    a ParityAccumulator add, median over `reps` calls."""
+    k, m, S = 10, 4, 4096
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = [torch.randint(0, 256, (S,), dtype=torch.uint8, device="cuda") for _ in range(k)]
+    coding = [torch.empty(S, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    acc = E.ParityAccumulator(m, S)
+    col = [M[i * k] for i in range(m)]
+    cases = {"jerasure_matrix_encode": lambda: E.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, S),
+             "jerasure_matrix_decode{0}": lambda: E.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, [0], data, coding,
+                                                                                    S),
+             "ParityAccumulator.add": lambda: acc.add(data[0], col)}
+    out = {}
+    for name, fn in cases.items():
+        for _ in range(10):
+            fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        out[name] = {"median_us": round(statistics.median(ts) * 1e6, 1), "p10_us": round(sorted(ts)[reps // 10] * 1e6, 1)}
+    acc.close()
+    return {"workload": "RS(10,4), 4 KiB device-resident shards, synchronous calls", "results": out}
+
+
 def device_configs():
     out = []
     cases = [("C2 RS(6,3) 1 MiB encode", 6, 3, 1 << 20, 96, None),
@@ -278,6 +307,7 @@ def main():
              "e2e_read_pipeline_4": lambda: e2e_read_pipeline([0, 1, 2, 3], a.stripes),
              "dropin_pageable": dropin_pageable,
              "ecx_accum": ecx_accum,
+             "call_latency": call_latency,
              "device_configs": device_configs}
     want = a.parts.split(",") if a.parts else list(parts)
     res = {name: parts[name]() for name in want}

@@ -16,9 +16,15 @@ extern "C" {
 ECGPU_API const char* ecgpu_version(void) { return "ecgpu 0.1 (gfx950)"; }
 ECGPU_API void ecgpu_free(void* p) { std::free(p); }
 
+constexpr int64_t kShardSkew = 10240;
+
 ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size) {
   if (size < 0) size = 0;
-  return ((size + 255) & ~int64_t(255)) + 4096;
+  // skew = 10 KiB (an odd multiple of 2 KiB): the shard-size x skew sweep on
+  // MI355X (profiles/r01_stride_sweep.jsonl) found every
+  // power-of-two-multiple skew bad at SOME shard size (4 KiB at 1 and 3 MiB
+  // shards: -10 %; 8 KiB at 2 MiB: -15 %), 6 and 10 KiB at none
+  return ((size + 255) & ~int64_t(255)) + kShardSkew;
 }
 
 ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w) { return single_multiply(a, b, w); }

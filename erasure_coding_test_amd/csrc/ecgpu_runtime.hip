@@ -676,7 +676,7 @@ struct ecgpu_accum {
   int device = 0, m = 0;
   int64_t size = 0;
   size_t slot = 0;
-  uint8_t* d_acc = nullptr;  // m slots, each `slot` bytes (4 KiB-skewed stride)
+  uint8_t* d_acc = nullptr;  // m slots, each `slot` bytes (skewed shard stride)
   std::vector<char> init;
 };
 
@@ -689,7 +689,7 @@ ECGPU_API ecgpu_accum* ecgpu_accum_create(int m, int64_t size, int device) {
   a->device = device < 0 ? current_device() : device;
   a->m = m;
   a->size = size;
-  a->slot = size_t(((size + 255) & ~int64_t(255)) + 4096);
+  a->slot = size_t(ecgpu_recommended_shard_stride(size));
   a->init.assign(size_t(m), 0);
   DeviceGuard g(a->device);
   hipError_t e = hipMalloc(reinterpret_cast<void**>(&a->d_acc), a->slot * size_t(m));

@@ -139,7 +139,7 @@ def test_decode_plan_replays_reference_decode(golden, vectors):
 
 def test_recommended_stride():
     from erasure_coding_test_amd import _native as N
-    assert N.lib.ecgpu_recommended_shard_stride(4 << 20) == (4 << 20) + 4096
+    assert N.lib.ecgpu_recommended_shard_stride(4 << 20) == (4 << 20) + 10240
     assert N.lib.ecgpu_recommended_shard_stride(1) % 256 == 0
 
 

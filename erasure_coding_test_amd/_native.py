@@ -98,6 +98,14 @@ SIGNATURES = {
     "ecgpu_pipeline_wait": (c_int, [c_void_p, c_int64]),
     "ecgpu_pipeline_drain": (c_int, [c_void_p]),
     "ecgpu_pipeline_destroy": (None, [c_void_p]),
+    "ecgpu_pipeline_group_create": (c_void_p, [c_int, c_int, c_int_p, c_int64, c_int, c_int, c_int_p]),
+    "ecgpu_pipeline_group_create_decode": (c_void_p, [c_int, c_int, c_int, c_int_p, c_int, c_int_p, c_int64, c_int,
+                                                      c_int, c_int_p]),
+    "ecgpu_pipeline_group_submit": (c_int64, [c_void_p, c_void_pp, c_void_pp]),
+    "ecgpu_pipeline_group_wait": (c_int, [c_void_p, c_int64]),
+    "ecgpu_pipeline_group_drain": (c_int, [c_void_p]),
+    "ecgpu_pipeline_group_size": (c_int, [c_void_p]),
+    "ecgpu_pipeline_group_destroy": (None, [c_void_p]),
     "ecgpu_host_register": (c_int, [c_void_p, c_int64]),
     "ecgpu_host_unregister": (c_int, [c_void_p]),
     "ecgpu_accum_create": (c_void_p, [c_int, c_int64, c_int]),

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <list>
 #include <memory>
 #include <mutex>
@@ -935,6 +936,95 @@ ECGPU_API void ecgpu_pipeline_destroy(ecgpu_pipeline* p) {
   (void)ecgpu_pipeline_drain(p);
   pipeline_free(p);
 }
+
+// ---------------------------------------------- multi-device pipeline ----
+// Stripes are independent, so a process driving several GPUs
+// shards them round-robin: stripe t runs on member t % n as that member's
+// local ticket t / n.  No collective and no cross-device traffic; each member
+// is a complete single-device pipeline with its own ring and streams, and
+// the submit path only enqueues asynchronous work, so one host thread keeps
+// every device busy.
+struct ecgpu_pipeline_group {
+  std::vector<ecgpu_pipeline*> members;
+  int64_t next_ticket = 0;
+  std::mutex mu;
+};
+
+namespace {
+void group_free(ecgpu_pipeline_group* g) {
+  if (!g) return;
+  for (auto* p : g->members) ecgpu_pipeline_destroy(p);
+  delete g;
+}
+
+ecgpu_pipeline_group* group_build(int ndev, const int* devices, const std::function<ecgpu_pipeline*(int)>& make) {
+  if (ndev <= 0 || !devices) {
+    fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group: ndev > 0 and a device list required");
+    return nullptr;
+  }
+  auto* g = new ecgpu_pipeline_group();
+  for (int i = 0; i < ndev; ++i) {
+    ecgpu_pipeline* p = make(devices[i]);
+    if (!p) {  // make() left the message in ecgpu_last_error
+      group_free(g);
+      return nullptr;
+    }
+    g->members.push_back(p);
+  }
+  return g;
+}
+}  // namespace
+
+ECGPU_API ecgpu_pipeline_group* ecgpu_pipeline_group_create(int k, int m, const int* matrix, int64_t size, int depth,
+                                                            int ndev, const int* devices) {
+  return group_build(ndev, devices,
+                     [&](int dev) { return ecgpu_pipeline_create(k, m, matrix, size, depth, dev); });
+}
+
+ECGPU_API ecgpu_pipeline_group* ecgpu_pipeline_group_create_decode(int k, int m, int w, const int* matrix,
+                                                                   int row_k_ones, const int* erasures, int64_t size,
+                                                                   int depth, int ndev, const int* devices) {
+  return group_build(ndev, devices, [&](int dev) {
+    return ecgpu_pipeline_create_decode(k, m, w, matrix, row_k_ones, erasures, size, depth, dev);
+  });
+}
+
+ECGPU_API int64_t ecgpu_pipeline_group_submit(ecgpu_pipeline_group* g, char** data_ptrs, char** coding_ptrs) {
+  if (!g || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_submit: bad arguments");
+  std::lock_guard<std::mutex> lk(g->mu);
+  const int64_t t = g->next_ticket;
+  const int64_t n = int64_t(g->members.size());
+  const int64_t local = ecgpu_pipeline_submit(g->members[size_t(t % n)], data_ptrs, coding_ptrs);
+  if (local < 0) return local;
+  if (local != t / n) return fail(ECGPU_ERR, "ecgpu_pipeline_group_submit: member ticket out of sequence");
+  g->next_ticket = t + 1;
+  return t;
+}
+
+ECGPU_API int ecgpu_pipeline_group_wait(ecgpu_pipeline_group* g, int64_t ticket) {
+  if (!g || ticket < 0) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_wait: bad arguments");
+  int64_t next, n;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    next = g->next_ticket;
+    n = int64_t(g->members.size());
+  }
+  if (ticket >= next) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_wait: ticket not submitted");
+  return ecgpu_pipeline_wait(g->members[size_t(ticket % n)], ticket / n);
+}
+
+ECGPU_API int ecgpu_pipeline_group_drain(ecgpu_pipeline_group* g) {
+  if (!g) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_drain: null");
+  for (auto* p : g->members) {
+    const int rc = ecgpu_pipeline_drain(p);
+    if (rc != ECGPU_OK) return rc;
+  }
+  return ECGPU_OK;
+}
+
+ECGPU_API int ecgpu_pipeline_group_size(ecgpu_pipeline_group* g) { return g ? int(g->members.size()) : 0; }
+
+ECGPU_API void ecgpu_pipeline_group_destroy(ecgpu_pipeline_group* g) { group_free(g); }
 
 ECGPU_API int ecgpu_host_register(void* ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return fail(ECGPU_ERR_ARG, "ecgpu_host_register: bad arguments");

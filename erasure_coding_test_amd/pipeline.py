@@ -77,6 +77,69 @@ class HostPipeline:
             pass
 
 
+class HostPipelineGroup:
+    """Several GPUs from one process (ecgpu_pipeline_group_*): one
+    single-device pipeline per entry of ``devices`` (repeats allowed), stripe
+    ticket t on member t % len(devices).  Stripes are independent, so there is
+    no collective; the interface is HostPipeline's."""
+
+    def __init__(self, k: int, m: int, matrix: Sequence[int], size: int, devices: Sequence[int], depth: int = 3,
+                 _handle=None):
+        self.k, self.m, self.size = k, m, size
+        self.devices = list(devices)
+        self._g = _handle if _handle is not None else N.lib.ecgpu_pipeline_group_create(
+            k, m, N.int_array(matrix), size, depth, len(self.devices), N.int_array(self.devices))
+        if not self._g:
+            raise N.EcgpuError(f"ecgpu_pipeline_group_create failed: {N.last_error()}")
+        self._keep = {}
+
+    @classmethod
+    def decoder(cls, k: int, m: int, matrix: Sequence[int], erasures: Sequence[int], size: int,
+                devices: Sequence[int], row_k_ones: int = 0, depth: int = 3) -> "HostPipelineGroup":
+        """Raises EcgpuError where the reference decode would return -1."""
+        er = list(erasures)
+        if not er or er[-1] != -1:
+            er.append(-1)
+        devs = list(devices)
+        h = N.lib.ecgpu_pipeline_group_create_decode(k, m, 8, N.int_array(matrix), row_k_ones, N.int_array(er), size,
+                                                     depth, len(devs), N.int_array(devs))
+        if not h:
+            raise N.EcgpuError(f"ecgpu_pipeline_group_create_decode failed: {N.last_error()}")
+        return cls(k, m, matrix, size, devs, depth, _handle=h)
+
+    def submit(self, data_ptrs, coding_ptrs) -> int:
+        if len(data_ptrs) != self.k or len(coding_ptrs) != self.m:
+            raise ValueError("k data and m coding buffers required")
+        for b in list(data_ptrs) + list(coding_ptrs):
+            if getattr(b, "is_cuda", False):
+                raise ValueError("HostPipelineGroup takes host buffers")
+        t = N.lib.ecgpu_pipeline_group_submit(self._g, N.ptr_array(addrs(data_ptrs)), N.ptr_array(addrs(coding_ptrs)))
+        if t < 0:
+            raise N.EcgpuError(f"ecgpu_pipeline_group_submit failed ({t}): {N.last_error()}")
+        self._keep[t] = (data_ptrs, coding_ptrs)
+        return t
+
+    def wait(self, ticket: int) -> None:
+        N.check(N.lib.ecgpu_pipeline_group_wait(self._g, ticket), "ecgpu_pipeline_group_wait")
+        self._keep.pop(ticket, None)
+
+    def drain(self) -> None:
+        N.check(N.lib.ecgpu_pipeline_group_drain(self._g), "ecgpu_pipeline_group_drain")
+        self._keep.clear()
+
+    def close(self) -> None:
+        if getattr(self, "_g", None):
+            N.lib.ecgpu_pipeline_group_destroy(self._g)
+            self._g = None
+            self._keep.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def host_register(buf, nbytes: int = -1) -> None:
     """Page-lock a host buffer (numpy array) for asynchronous DMA."""
     n = buf.nbytes if nbytes < 0 else nbytes

@@ -204,6 +204,23 @@ ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, cha
 ECGPU_API int ecgpu_pipeline_wait(ecgpu_pipeline* p, int64_t ticket);
 ECGPU_API int ecgpu_pipeline_drain(ecgpu_pipeline* p);
 ECGPU_API void ecgpu_pipeline_destroy(ecgpu_pipeline* p);
+/* Several GPUs from one process: stripes are independent, so
+ * a group of single-device pipelines (one per entry of devices[], repeats
+ * allowed) takes them round-robin -- stripe ticket t runs on member t % ndev.
+ * No collective, no cross-device traffic; submit only enqueues asynchronous
+ * work, so one host thread drives every device.  Same buffer rules and
+ * results as ecgpu_pipeline_*; wait(t) returns once stripe t is complete. */
+typedef struct ecgpu_pipeline_group ecgpu_pipeline_group;
+ECGPU_API ecgpu_pipeline_group* ecgpu_pipeline_group_create(int k, int m, const int* matrix, int64_t size, int depth,
+                                                            int ndev, const int* devices);
+ECGPU_API ecgpu_pipeline_group* ecgpu_pipeline_group_create_decode(int k, int m, int w, const int* matrix,
+                                                                   int row_k_ones, const int* erasures, int64_t size,
+                                                                   int depth, int ndev, const int* devices);
+ECGPU_API int64_t ecgpu_pipeline_group_submit(ecgpu_pipeline_group* g, char** data_ptrs, char** coding_ptrs);
+ECGPU_API int ecgpu_pipeline_group_wait(ecgpu_pipeline_group* g, int64_t ticket);
+ECGPU_API int ecgpu_pipeline_group_drain(ecgpu_pipeline_group* g);
+ECGPU_API int ecgpu_pipeline_group_size(ecgpu_pipeline_group* g);
+ECGPU_API void ecgpu_pipeline_group_destroy(ecgpu_pipeline_group* g);
 /* Page-lock caller memory for asynchronous DMA (hipHostRegister). */
 ECGPU_API int ecgpu_host_register(void* ptr, int64_t bytes);
 ECGPU_API int ecgpu_host_unregister(void* ptr);

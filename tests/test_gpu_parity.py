@@ -529,6 +529,59 @@ def test_host_pipeline_decoder_rejects_undecodable(ec, gpu):
         ec.HostPipeline.decoder(6, 3, M, [0, 1, 2, 3], 4096)
 
 
+# ------------------------------------ multi-device group (one process) ----
+# The one-GPU box repeats device 0 in the member list: the round-robin
+# ticket mapping, per-member rings and out-of-order waits are what is tested
+# here; members on distinct devices differ only in the device ordinal.
+@pytest.mark.parametrize("members", [1, 2, 3])
+def test_pipeline_group_encode_round_robin(ec, gpu, restatement, members):
+    import torch
+    k, m, size, stripes = 10, 4, (1 << 18) + 7, 8
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = [[torch.from_numpy(b).pin_memory() for b in host_shards(60, s, k, size)] for s in range(stripes)]
+    coding = [[torch.zeros(size + PAD, dtype=torch.uint8).pin_memory() for _ in range(m)] for _ in range(stripes)]
+    g = ec.HostPipelineGroup(k, m, M, size, devices=[0] * members, depth=2)
+    assert ec._native.lib.ecgpu_pipeline_group_size(g._g) == members
+    tickets = [g.submit(data[s], coding[s]) for s in range(stripes)]
+    assert tickets == list(range(stripes))
+    g.wait(tickets[-1])  # a late member's ticket first, then an early one
+    g.wait(tickets[1])
+    g.drain()
+    with pytest.raises(ec._native.EcgpuError):
+        g.wait(stripes)  # never submitted
+    g.close()
+    for s in range(stripes):
+        ref = _encode_ref(restatement, k, m, M, [b.numpy() for b in data[s]], size)
+        for i in range(m):
+            assert np.array_equal(coding[s][i].numpy()[:size], ref[i][:size]), (s, i)
+            assert not coding[s][i].numpy()[size:].any()
+
+
+def test_pipeline_group_decoder(ec, gpu):
+    import torch
+    k, m, size, stripes = 6, 3, (1 << 16) + 1, 5
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    full, want = [], []
+    for s in range(stripes):
+        d, c = host_shards(61, s, k, size), alloc_shards(m, size, PAD)
+        ec.jerasure.jerasure_matrix_encode(k, m, 8, M, d, c, size)
+        full.append([torch.from_numpy(b).pin_memory() for b in d + c])
+        want.append([b.copy() for b in d + c])
+    for st in full:
+        for e in (1, 7):
+            st[e].fill_(0x5A)
+    g = ec.HostPipelineGroup.decoder(k, m, M, [1, 7], size, devices=[0, 0])
+    for st in full:
+        g.submit(st[:k], st[k:])
+    g.drain()
+    g.close()
+    for s in range(stripes):
+        for i in range(k + m):
+            assert np.array_equal(full[s][i].numpy()[:size], want[s][i][:size]), (s, i)
+    with pytest.raises(ec._native.EcgpuError):
+        ec.HostPipelineGroup.decoder(k, m, M, [0, 1, 2, 3], size, devices=[0, 0])
+
+
 # ------------------------------------------- wide words (w = 16 / 32) ----
 def _ref_nsa():
     import ctypes

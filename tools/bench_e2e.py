@@ -112,13 +112,16 @@ def e2e_pinned(stripes=48, k=10, m=4, S=4 << 20, ring=3):
             "h2d_GBps": round(stripes * k * S / t / 1e9, 1), "parity_ok": ok}
 
 
-def e2e_pipeline(stripes=48, k=10, m=4, S=4 << 20, depth=3, pinned=True):
+def e2e_pipeline(stripes=48, k=10, m=4, S=4 << 20, depth=3, pinned=True, devices=None):
+    """devices: None = HostPipeline on the current device; a list = the
+    multi-device HostPipelineGroup over those ordinals (round-robin stripes)."""
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     host = torch.empty((stripes, k + m, S), dtype=torch.uint8)
     if pinned:
         host = host.pin_memory()
     host[:, :k].random_(0, 256)
-    p = E.HostPipeline(k, m, M, S, depth=depth)
+    p = E.HostPipeline(k, m, M, S, depth=depth) if devices is None else E.HostPipelineGroup(
+        k, m, M, S, devices=devices, depth=depth)
 
     def run():
         for s in range(stripes):
@@ -135,7 +138,8 @@ def e2e_pipeline(stripes=48, k=10, m=4, S=4 << 20, depth=3, pinned=True):
     E.encode_plan(k, m, M).bind([[d[j] for j in range(k)]], [[ref[i] for i in range(m)]], S).launch()
     torch.cuda.synchronize()
     ok = bool(torch.equal(ref.cpu(), host[stripes - 1, k:]))
-    return {"workload": f"RS(10,4) 4 MiB encode via ecgpu_pipeline, {stripes} stripes "
+    via = "ecgpu_pipeline" if devices is None else f"ecgpu_pipeline_group over devices {devices}"
+    return {"workload": f"RS(10,4) 4 MiB encode via {via}, {stripes} stripes "
                         f"{'pinned' if pinned else 'pageable'} host, depth {depth}",
             "data_GiBps": round(stripes * k * S / t / GiB, 2), "parity_ok": ok}
 
@@ -303,6 +307,9 @@ def main():
     parts = {"pcie": pcie_rates, "e2e_pinned": lambda: e2e_pinned(a.stripes),
              "e2e_pipeline_pinned": lambda: e2e_pipeline(a.stripes),
              "e2e_pipeline_pageable": lambda: e2e_pipeline(a.stripes, pinned=False),
+             "e2e_group_all_devices": lambda: e2e_pipeline(
+                 a.stripes, devices=list(range(torch.cuda.device_count()))),
+             "e2e_group_dev0_twice": lambda: e2e_pipeline(a.stripes, devices=[0, 0]),
              "e2e_read_pipeline_1": lambda: e2e_read_pipeline([0], a.stripes),
              "e2e_read_pipeline_4": lambda: e2e_read_pipeline([0, 1, 2, 3], a.stripes),
              "dropin_pageable": dropin_pageable,

@@ -845,3 +845,83 @@ def test_schedule_decode_lazy_and_cache_device(ec, gpu, smart):
                 assert torch.equal(t, orig[i]), (er, method, i)
     assert cache.decode([0, 1, 2], data, coding, size, ps) == -1
     cache.close()
+
+
+# ------------------------------------------- randomized (seeded) cases ----
+# Arbitrary fused maps through the batched plan API, checked against the
+# reference's own 256 x 256 product table (tests/golden vectors.npz): random
+# source counts (1..20, so both the specialised K <= 16 kernels and the
+# generic one), 1..7 output rows (several launches), densities of zero /
+# unit / general coefficients, ragged sizes, 0..15-byte misaligned buffers.
+def _random_map_case(seed):
+    rng = np.random.default_rng(7000 + seed)
+    K, R, stripes = int(rng.integers(1, 21)), int(rng.integers(1, 8)), int(rng.integers(1, 4))
+    size = int(rng.choice([1, 15, 16, 17, 4096, (1 << 16) + 48, int(rng.integers(1, 200_000))]))
+    kind = rng.choice(3, size=(R, K), p=[0.15, 0.25, 0.6])
+    coefs = np.where(kind == 0, 0, np.where(kind == 1, 1, rng.integers(2, 256, size=(R, K))))
+    offs = rng.integers(0, 16, size=(stripes, K + R)) if seed % 3 == 0 else np.zeros((stripes, K + R), np.int64)
+    return rng, K, R, stripes, size, coefs.astype(np.int64), offs
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_fused_maps_vs_reference_table(ec, gpu, vectors, seed):
+    import torch
+    T = vectors["gf_mul_table"].reshape(256, 256)
+    rng, K, R, stripes, size, coefs, offs = _random_map_case(seed)
+    host_src = [[rng.integers(0, 256, size, dtype=np.uint8) for _ in range(K)] for _ in range(stripes)]
+    bufs, srcs, dsts = [], [], []
+    for s in range(stripes):
+        row_s, row_d = [], []
+        for j in range(K + R):
+            o = int(offs[s, j])
+            b = torch.full((o + size + PAD,), 0xCC, dtype=torch.uint8, device=gpu)
+            bufs.append(b)
+            v = b[o:o + size]
+            if j < K:
+                v.copy_(torch.from_numpy(host_src[s][j]))
+                row_s.append(v)
+            else:
+                row_d.append(v)
+        srcs.append(row_s)
+        dsts.append(row_d)
+    p = ec.plan.StripePlan(R, K, coefs.ravel().tolist()).bind(srcs, dsts, size)
+    p.launch()
+    torch.cuda.synchronize()
+    for s in range(stripes):
+        for r in range(R):
+            want = np.zeros(size, np.uint8)
+            for j in range(K):
+                want ^= T[coefs[r, j]][host_src[s][j]]
+            b = bufs[s * (K + R) + K + r].cpu().numpy()
+            o = int(offs[s, K + r])
+            assert np.array_equal(b[o:o + size], want), (seed, K, R, size, s, r)
+            assert (b[:o] == 0xCC).all() and (b[o + size:] == 0xCC).all(), "wrote outside the region"
+    p.close()
+
+
+# jerasure_matrix_decode on random (k, m, erasures, row_k_ones) against the
+# reference library compiled from /root/reference (oracle/_ref): decoded
+# bytes must equal the reference decode on the same inputs, and the return
+# code must match (including undecodable patterns).
+@pytest.mark.parametrize("seed", range(24))
+def test_random_decode_vs_reference(ec, gpu, reference, seed):
+    rng = np.random.default_rng(9000 + seed)
+    k, m = int(rng.integers(2, 15)), int(rng.integers(1, 7))
+    size = 8 * int(rng.integers(1, 8192))  # whole 8-byte words: the reference's loops over-run otherwise
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    ne = int(rng.integers(1, m + 2))  # up to m + 1 erasures: the last may be undecodable
+    erasures = sorted(int(x) for x in rng.choice(k + m, size=min(ne, k + m), replace=False))
+    row_k_ones = int(rng.integers(0, 2))
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)]
+    coding = [np.zeros(size, np.uint8) for _ in range(m)]
+    reference.matrix_encode(k, m, np.array(M).reshape(m, k), data, coding, size)
+    for e in erasures:  # scribble over the erased shards
+        (data + coding)[e][:] = rng.integers(0, 256, size, dtype=np.uint8)
+    ref_bufs = [b.copy() for b in data + coding]
+    got_bufs = [b.copy() for b in data + coding]
+    rc_ref = reference.matrix_decode(k, m, np.array(M).reshape(m, k), row_k_ones, erasures, ref_bufs[:k],
+                                     ref_bufs[k:], size)
+    rc_got = ec.jerasure.jerasure_matrix_decode(k, m, 8, M, row_k_ones, erasures, got_bufs[:k], got_bufs[k:], size)
+    assert rc_got == rc_ref, (k, m, erasures, row_k_ones)
+    for i in range(k + m):
+        assert np.array_equal(got_bufs[i], ref_bufs[i]), (k, m, erasures, row_k_ones, i)

@@ -13,7 +13,9 @@
 // sizeof(long)); a ragged size, where the reference reads and writes past the
 // region, takes the exact-word CPU restatement in jerasure_surface.cpp.
 // Host-side math (fields, matrices) comes from libecgpu's host C ABI.
-// Bit-matrix / schedule coding is CPU code in jerasure_surface.cpp.
+// Bit-matrix / schedule coding lives in jerasure_surface.cpp: execution on
+// the MI355X (GF(2) packet kernels), matrix / schedule construction on the
+// host.
 #include <cstdio>
 #include <cstdlib>
 

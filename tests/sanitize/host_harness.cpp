@@ -1,0 +1,143 @@
+// host_harness.cpp -- drives the HOST-ONLY part of libecgpu (field tables,
+// matrix construction / inversion, the decode planner, bit-matrix and
+// schedule construction; csrc/{gf_host,matrix_host,planner,schedule_host,
+// capi_host}.cpp) under AddressSanitizer + UBSan, or ThreadSanitizer with
+// `threads` > 1 (first-use table initialisation races between callers).
+// Built and run by tests/test_sanitizers.py.  No GPU code is linked: the one
+// device entry point the host objects reference is stubbed and never called.
+//
+//   host_harness [threads]      exit 0 = every check passed, sanitizer clean
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "ecgpu.h"
+
+extern "C" int ecgpu_schedule_run(int, char**, int**, int, int, int) {
+  std::fprintf(stderr, "ecgpu_schedule_run: GPU entry point called from the host harness\n");
+  std::abort();
+}
+
+namespace {
+
+int failures = 0;
+
+void expect(bool ok, const char* what, int a = 0, int b = 0) {
+  if (!ok) {
+    std::fprintf(stderr, "FAIL %s (%d, %d)\n", what, a, b);
+    __atomic_add_fetch(&failures, 1, __ATOMIC_RELAXED);
+  }
+}
+
+// Known answers from the reference.
+void known_answers() {
+  expect(ecgpu_galois_single_multiply(2, 0x80, 8) == 29, "mul(2,0x80)");
+  expect(ecgpu_galois_single_multiply(3, 7, 8) == 9, "mul(3,7)");
+  expect(ecgpu_galois_inverse(2, 8) == 142, "inverse(2)");
+  expect(ecgpu_galois_single_divide(1, 147, 8) == 79, "div(1,147)");
+  int* M = ecgpu_reed_sol_vandermonde_coding_matrix(10, 4, 8);
+  const int row1[10] = {1, 147, 138, 73, 93, 161, 103, 58, 99, 178};
+  expect(M && std::memcmp(M + 10, row1, sizeof(row1)) == 0, "RS(10,4) row 1");
+  std::free(M);
+}
+
+void matrices() {
+  for (int w : {8, 16, 32})
+    for (int k = 2; k <= 16; ++k)
+      for (int m = 1; m <= 8; ++m) {
+        if (w == 8 && k + m > 256) continue;
+        int* M = ecgpu_reed_sol_vandermonde_coding_matrix(k, m, w);
+        expect(M != nullptr, "vandermonde", k, m);
+        if (!M) continue;
+        for (int j = 0; j < k; ++j) expect(M[j] == 1, "row 0 all ones", k, j);
+        for (int i = 0; i < m; ++i) expect(M[i * k] == 1, "column 0 all ones", k, i);
+        // the bit-matrix image and its two-erasure decoding bit-matrix
+        if (w == 8 && m >= 2) {
+          int* B = ecgpu_jerasure_matrix_to_bitmatrix(k, m, w, M);
+          std::vector<int> erased(static_cast<size_t>(k + m), 0), dm(static_cast<size_t>(k * k * w * w)),
+              ids(static_cast<size_t>(k));
+          erased[0] = erased[1] = 1;
+          expect(ecgpu_jerasure_make_decoding_bitmatrix(k, m, w, B, erased.data(), dm.data(), ids.data()) == 0,
+                 "decoding bitmatrix", k, m);
+          int** dumb = ecgpu_jerasure_dumb_bitmatrix_to_schedule(k, m, w, B);
+          int** smart = ecgpu_jerasure_smart_bitmatrix_to_schedule(k, m, w, B);
+          expect(dumb && smart, "schedules", k, m);
+          ecgpu_jerasure_free_schedule(dumb);
+          ecgpu_jerasure_free_schedule(smart);
+          if (m == 2 && k <= 8) {
+            int*** cache = ecgpu_jerasure_generate_schedule_cache(k, m, w, B, 1);
+            expect(cache != nullptr, "schedule cache", k, m);
+            expect(ecgpu_jerasure_free_schedule_cache(k, m, cache) == 0, "free schedule cache", k, m);
+          }
+          std::free(B);
+        }
+        std::free(M);
+      }
+}
+
+// Every erasure pattern of RS(10,4) up to 5 erasures (5 = undecodable) and
+// row_k_ones 0/1, through the fused decode planner; inversion round trips.
+void decode_plans() {
+  const int k = 10, m = 4, n = k + m;
+  int* M = ecgpu_reed_sol_vandermonde_coding_matrix(k, m, 8);
+  std::vector<int> out(static_cast<size_t>(n)), src(static_cast<size_t>(n)), coef(static_cast<size_t>(n * n));
+  int patterns = 0;
+  for (int mask = 1; mask < (1 << n); ++mask) {
+    const int ne = __builtin_popcount(unsigned(mask));
+    if (ne > m + 1) continue;
+    std::vector<int> er;
+    for (int i = 0; i < n; ++i)
+      if (mask >> i & 1) er.push_back(i);
+    er.push_back(-1);
+    for (int rko = 0; rko < 2; ++rko) {
+      int n_out = 0, n_src = 0;
+      const int rc = ecgpu_decode_plan(k, m, 8, M, rko, er.data(), out.data(), &n_out, src.data(), &n_src,
+                                       coef.data());
+      expect(ne <= m ? rc == 0 : rc != 0, "decode plan rc", mask, rc);
+      if (rc == 0) expect(n_out == ne && n_src <= k, "decode plan shape", n_out, n_src);
+      ++patterns;
+    }
+  }
+  expect(patterns > 2000, "pattern count", patterns);
+  // inversion of every k x k survivor matrix of RS(6,3) with 3 erasures
+  int* M63 = ecgpu_reed_sol_vandermonde_coding_matrix(6, 3, 8);
+  std::vector<int> erased(9), dm(36), ids(6);
+  for (int a = 0; a < 9; ++a)
+    for (int b = a + 1; b < 9; ++b)
+      for (int c = b + 1; c < 9; ++c) {
+        std::fill(erased.begin(), erased.end(), 0);
+        erased[size_t(a)] = erased[size_t(b)] = erased[size_t(c)] = 1;
+        expect(ecgpu_jerasure_make_decoding_matrix(6, 3, 8, M63, erased.data(), dm.data(), ids.data()) == 0,
+               "RS(6,3) decoding matrix", a * 100 + b * 10 + c);
+      }
+  std::free(M63);
+  std::free(M);
+}
+
+void run_all() {
+  known_answers();
+  matrices();
+  decode_plans();
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int threads = argc > 1 ? std::atoi(argv[1]) : 1;
+  if (threads <= 1) {
+    run_all();
+  } else {
+    // concurrent first use of the lazily built field tables and the planner
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) ts.emplace_back(run_all);
+    for (auto& t : ts) t.join();
+  }
+  if (failures) {
+    std::fprintf(stderr, "%d check(s) failed\n", failures);
+    return 1;
+  }
+  std::printf("host harness ok (%d thread(s))\n", threads);
+  return 0;
+}

@@ -433,6 +433,8 @@ struct Ctx {
   hipStream_t stream = nullptr;
   uint8_t* stage = nullptr;
   size_t stage_cap = 0;
+  uint8_t* bounce = nullptr;  // pinned host mirror of the staging slab (small calls, see execute)
+  size_t bounce_cap = 0;
   std::list<std::pair<PlanKey, ecgpu_plan*>> plans;  // LRU, front = newest
 };
 
@@ -506,6 +508,29 @@ int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int 
     c->plans.pop_back();
   }
   *out = p;
+  return ECGPU_OK;
+}
+
+// Small synchronous calls on host buffers: every pageable hipMemcpyAsync
+// pays a fixed staging cost (~10 us each, six of them for RS(4,2)), so up to
+// kBounceMax staged bytes the host side is copied by the CPU through one
+// pinned mirror of the staging slab and crosses PCIe as ONE H2D DMA (inputs)
+// plus one D2H DMA per output.  Above it HIP's pipelined pageable copies win.
+constexpr size_t kBounceMax = size_t(2) << 20;
+
+size_t bounce_max() {
+  static const size_t v = size_t(env_int("ECGPU_BOUNCE_KIB", int(kBounceMax >> 10))) << 10;
+  return v;
+}
+
+int ensure_bounce(Ctx* c, size_t bytes) {
+  if (bytes <= c->bounce_cap) return ECGPU_OK;
+  DeviceGuard g(c->device);
+  if (c->bounce) ECGPU_HIP(hipHostFree(c->bounce));
+  c->bounce = nullptr;
+  c->bounce_cap = 0;
+  ECGPU_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->bounce), bytes, hipHostMallocDefault));
+  c->bounce_cap = bytes;
   return ECGPU_OK;
 }
 
@@ -593,9 +618,22 @@ int execute(const FusedOp& op, int64_t size) {
   size_t next = 0;
   for (size_t i = 0; i < bufs.size(); ++i)
     if (staged[i]) devp[i] = c->stage + (next++) * slot;
+  // Staged sources take the first staging slots (bufs lists sources first),
+  // so with the pinned bounce they go up as one contiguous DMA.
+  const bool bounce = nstage > 0 && nstage * slot <= bounce_max();
+  if (bounce && (rc = ensure_bounce(c, nstage * slot)) != ECGPU_OK) return rc;
+  auto bounce_of = [&](size_t i) { return c->bounce + (devp[i] - c->stage); };
+  size_t staged_src = 0;
   for (size_t j = 0; j < op.srcs.size(); ++j)
-    if (staged[j])
-      ECGPU_HIP(hipMemcpyAsync(devp[j], op.srcs[j], size_t(size), hipMemcpyHostToDevice, c->stream));
+    if (staged[j]) {
+      ++staged_src;
+      if (bounce)
+        std::memcpy(bounce_of(j), op.srcs[j], size_t(size));
+      else
+        ECGPU_HIP(hipMemcpyAsync(devp[j], op.srcs[j], size_t(size), hipMemcpyHostToDevice, c->stream));
+    }
+  if (bounce && staged_src > 0)
+    ECGPU_HIP(hipMemcpyAsync(c->stage, c->bounce, staged_src * slot, hipMemcpyHostToDevice, c->stream));
 
   std::vector<const uint8_t*> sp(static_cast<size_t>(nsrc));
   std::vector<uint8_t*> dp(static_cast<size_t>(rows));
@@ -622,10 +660,16 @@ int execute(const FusedOp& op, int64_t size) {
     if (via_temp)
       ECGPU_HIP(hipMemcpyAsync(devp[i], dp[r], size_t(size), hipMemcpyDeviceToDevice, c->stream));
     if (staged[i])
-      ECGPU_HIP(hipMemcpyAsync(op.dsts[r], devp[i], size_t(size), hipMemcpyDeviceToHost, c->stream));
+      ECGPU_HIP(hipMemcpyAsync(bounce ? static_cast<void*>(bounce_of(i)) : op.dsts[r], devp[i], size_t(size),
+                               hipMemcpyDeviceToHost, c->stream));
   }
   ECGPU_HIP(hipStreamSynchronize(c->stream));
   ECGPU_HIP(hipGetLastError());
+  if (bounce)
+    for (int r = 0; r < rows; ++r) {
+      const size_t i = size_t(std::find(bufs.begin(), bufs.end(), op.dsts[r]) - bufs.begin());
+      if (staged[i]) std::memcpy(op.dsts[r], bounce_of(i), size_t(size));
+    }
   return ECGPU_OK;
 }
 

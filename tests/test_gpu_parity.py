@@ -219,21 +219,48 @@ def test_misaligned_buffers(ec, gpu, restatement, offset):
         assert np.array_equal(a.cpu().numpy(), b[:size])
 
 
-def test_aliased_coding_buffers_follow_sequential_semantics(ec, gpu, restatement):
+@pytest.mark.parametrize("where,size", [("device", 5000), ("host", 5000), ("host", 300_001)])
+def test_aliased_coding_buffers_follow_sequential_semantics(ec, gpu, restatement, where, size):
     # coding[0] aliases data[2]: the reference overwrites data[2] with parity 0
     # before computing parity 1..; the fused plan must reproduce that exactly.
-    k, m, size = 6, 6, 5000
+    # m = 6 > 4 rows: two launches, outputs through temporaries.  Host buffers
+    # take the pinned bounce (small) or per-buffer pageable copies (large).
+    k, m = 6, 6
     M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     hdata = host_shards(32, 0, k, size)
     hcoding = alloc_shards(m, size, PAD)
     hcoding[0] = hdata[2]
     restatement.matrix_encode(k, m, np.array(M).reshape(m, k), hdata, hcoding, size)
     ref = [x.copy() for x in hdata + hcoding[1:]]
-    dd = to_dev(host_shards(32, 0, k, size), gpu)
-    dc = [dd[2]] + to_dev(alloc_shards(m - 1, size, PAD), gpu)
+    if where == "device":
+        dd = to_dev(host_shards(32, 0, k, size), gpu)
+        dc = [dd[2]] + to_dev(alloc_shards(m - 1, size, PAD), gpu)
+    else:
+        dd = host_shards(32, 0, k, size)
+        dc = [dd[2]] + alloc_shards(m - 1, size, PAD)
     ec.jerasure.jerasure_matrix_encode(k, m, 8, M, dd, dc, size)
-    for a, b in zip(to_host(dd + dc[1:]), ref):
+    got = to_host(dd + dc[1:]) if where == "device" else dd + dc[1:]
+    for a, b in zip(got, ref):
         assert np.array_equal(a[:size], b[:size])
+
+
+@pytest.mark.parametrize("size", [4096, 1 << 20, 3 << 20])
+def test_host_region_ops_aliasing(ec, gpu, restatement, size):
+    """Region ops on pageable host buffers, in place and aliased, on both sides
+    of the pinned-bounce threshold (2 MiB of staged bytes)."""
+    a0, b0 = host_shards(33, 0, 2, size)
+    a, b = a0.copy(), b0.copy()
+    ra, rb = a0.copy(), b0.copy()
+    ec.galois.galois_region_xor(a, b, a, size)  # r3 aliases r1
+    restatement.region_xor(ra, rb, ra, size)
+    assert np.array_equal(a[:size], ra[:size])
+    ec.galois.galois_w08_region_multiply(b, 0x8E, size, None, 0)  # in place
+    restatement.region_multiply(rb, 0x8E, size, None, 0)
+    assert np.array_equal(b[:size], rb[:size])
+    ec.galois.galois_w08_region_multiply(a, 0x1D, size, b, 1)  # b ^= 0x1D * a
+    restatement.region_multiply(ra, 0x1D, size, rb, 1)
+    assert np.array_equal(b[:size], rb[:size])
+    assert np.array_equal(a[size:], a0[size:]) and np.array_equal(b[size:], b0[size:])  # padding untouched
 
 
 def test_decode_plan_batch_matches_jerasure(ec, gpu):

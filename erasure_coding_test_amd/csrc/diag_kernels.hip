@@ -9,6 +9,8 @@
 //              lane, nothing written)
 //   variant 13 / 14: production combine, register / LDS-DMA loads, explicit
 //              nt bits (loads / stores)
+//   variant 15: production combine with inline-asm loads / stores carrying
+//              explicit sc0 / sc1 / nt cache bits (cache-policy probe)
 //   variant 10: production gf_apply with the round-1 2-bit-slice tables
 //              (A/B against variants 4/8, which use the 3-bit-slice ptab)
 #include <hip/hip_runtime.h>
@@ -30,6 +32,81 @@ namespace {
 __device__ __forceinline__ void sink(const ApplyArgs& a, int s, int64_t col, const u32x4& acc) {
   if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u && acc.z == 0x85EBCA6Bu && acc.w == 0xC2B2AE35u)
     ecgpu::dev::store16(a.dst[int64_t(s) * a.dst_stride], col, acc, 1);
+}
+
+// ---- cache-policy probe (variant 15): the production combine with loads
+// and stores issued by inline asm carrying explicit gfx950 cache bits
+// (sc0 / sc1 / nt), beyond what __builtin_nontemporal_* can express.
+// Loads: 0 "nt", 1 "sc1 nt", 2 "sc0 sc1 nt", 3 "sc0 sc1", 4 "sc1".
+// Stores: 0 "nt", 1 "sc1", 2 "sc0 sc1", 3 "sc0 sc1 nt", 4 "sc1 nt".
+template <int LP>
+__device__ __forceinline__ u32x4 asm_load16(const uint8_t* p) {
+  u32x4 v;
+  if constexpr (LP == 0) asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+  if constexpr (LP == 1) asm volatile("global_load_dwordx4 %0, %1, off sc1 nt" : "=v"(v) : "v"(p) : "memory");
+  if constexpr (LP == 2) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt" : "=v"(v) : "v"(p) : "memory");
+  if constexpr (LP == 3) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(v) : "v"(p) : "memory");
+  if constexpr (LP == 4) asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// Each store is followed by s_nop 1: a VALU write to the data VGPRs of an
+// in-flight store wider than 8 bytes needs wait states, which the compiler's
+// hazard recognizer inserts for its own stores but not after inline asm
+// (without them the next VALU op corrupted the stored data).
+template <int SP>
+__device__ __forceinline__ void asm_store16(uint8_t* p, const u32x4& v) {
+  if constexpr (SP == 0) asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+  if constexpr (SP == 1) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+  if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+  if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+  if constexpr (SP == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+}
+
+template <int K, int R, int UNITS, int LP, int SP>
+__global__ __launch_bounds__(256) void gf_apply_pol(ApplyArgs a) {
+  const int64_t col = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  const uint8_t* src[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) src[j] = sp[j];
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = asm_load16<LP>(src[j] + col * 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int j = 0; j < K; ++j) asm volatile("" : "+v"(x[j]));  // uses stay after the wait
+  u32x4 acc[R];
+  ecgpu::dev::combine<K, R, UNITS, 3>(a, x, acc);
+#pragma unroll
+  for (int r = 0; r < R; ++r) asm_store16<SP>(dp[r] + col * 16, acc[r]);
+}
+
+template <int K, int R, int U, int LP>
+KernelFn pick_sp(int sp) {
+  switch (sp) {
+    case 0: return &gf_apply_pol<K, R, U, LP, 0>;
+    case 1: return &gf_apply_pol<K, R, U, LP, 1>;
+    case 2: return &gf_apply_pol<K, R, U, LP, 2>;
+    case 3: return &gf_apply_pol<K, R, U, LP, 3>;
+    default: return &gf_apply_pol<K, R, U, LP, 4>;
+  }
+}
+
+template <int K, int R, int U>
+KernelFn pick_pol(int lp, int sp) {
+  switch (lp) {
+    case 0: return pick_sp<K, R, U, 0>(sp);
+    case 1: return pick_sp<K, R, U, 1>(sp);
+    case 2: return pick_sp<K, R, U, 2>(sp);
+    case 3: return pick_sp<K, R, U, 3>(sp);
+    default: return pick_sp<K, R, U, 4>(sp);
+  }
 }
 
 // K register loads per lane (the production kernel's load phase).
@@ -180,6 +257,12 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
     if (K == 4) fn = nt ? &diag_read_glds<4, 1> : &diag_read_glds<4, 0>;
     if (K == 10) fn = nt ? &diag_read_glds<10, 1> : &diag_read_glds<10, 0>;
     if (K == 14) fn = nt ? &diag_read_glds<14, 1> : &diag_read_glds<14, 0>;
+  } else if (variant == 15) {
+    // cache-policy probe: vec = load policy, mode = store policy (gf_apply_pol)
+    const int lp = vec;
+    vec = 1;
+    if (K == 10 && R == 4) fn = pick_pol<10, 4, 3>(lp, mode);
+    if (K == 10 && R == 1) fn = pick_pol<10, 1, 4>(lp, mode);
   } else if (variant == 2) {
     vec = 1;
     if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_lds<10, 4>;

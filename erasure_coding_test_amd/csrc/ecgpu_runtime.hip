@@ -124,8 +124,9 @@ unsigned residency_lds_bytes(int device) {
 //   * residency cap unless the launch is dense in GF multiplies (more than
 //     2.5 non-unit coefficients per shard touched): decode{0} +9 %, RS(6,3)
 //     +6 %; the 40-multiply decode{0,1,2,3} needs the occupancy (-7 % capped).
-// The store policy is the plan's `nt` flag (ECGPU_NT, ecgpu_plan_set_kernel;
-// default 1); ECGPU_CAP (0 = never, 1 = always) overrides the cap rule.
+// The store policy is the plan's `nt` field (0 plain, 1 nt -- the default --
+// 2 sc1, 3 sc0 sc1; ECGPU_NT, ecgpu_plan_set_kernel); ECGPU_CAP (0 = never,
+// 1 = always) overrides the cap rule.
 bool cap_for(int K, int R, int mul_terms) {
   static const int v = env_int("ECGPU_CAP", -1);
   return v < 0 ? 2 * mul_terms <= 5 * (K + R) : (v != 0);
@@ -241,7 +242,7 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
   p->nsrc = nsrc;
   p->w = w;
   p->kind = env_int("ECGPU_KERNEL", ECGPU_KERNEL_PERM);
-  p->nt = env_int("ECGPU_NT", 1);
+  p->nt = std::min(kStorePolicies - 1, std::max(0, env_int("ECGPU_NT", 1)));
   const size_t n = size_t(rows) * nsrc;
   p->coef.resize(n);
   if (w != 8) {
@@ -705,7 +706,7 @@ ECGPU_API int ecgpu_plan_set_kernel(ecgpu_plan* p, int kind, int nontemporal) {
   if (!p || (kind != ECGPU_KERNEL_PERM && kind != ECGPU_KERNEL_LDS))
     return fail(ECGPU_ERR_ARG, "ecgpu_plan_set_kernel: bad arguments");
   p->kind = kind;
-  p->nt = nontemporal ? 1 : 0;
+  p->nt = std::min(kStorePolicies - 1, std::max(0, nontemporal));
   return ECGPU_OK;
 }
 

@@ -93,11 +93,24 @@ __device__ __forceinline__ u32x4 load16t(const uint8_t* p, int64_t col) {
   else return *a;
 }
 
-template <int NT>
+// Store cache policy POL: 0 plain, 1 non-temporal (`nt`), 2 `sc1`, 3
+// `sc0 sc1` (written through, not kept in the XCD's L2: MI355X_MICROARCH.md
+// "stores of each flavour").  No builtin expresses sc0/sc1, so 2 and 3 are
+// inline-asm vector stores followed by s_nop 1: a VALU write to the data
+// VGPRs of an in-flight store wider than 8 bytes needs wait states, which the
+// compiler inserts after its own stores but not after inline asm.
+template <int POL>
 __device__ __forceinline__ void store16t(uint8_t* p, int64_t col, const u32x4& v) {
   gu32x4* a = (gu32x4*)p + col;
-  if constexpr (NT != 0) __builtin_nontemporal_store(v, a);
-  else *a = v;
+  if constexpr (POL == 3) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(p + col * 16), "v"(v) : "memory");
+  } else if constexpr (POL == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p + col * 16), "v"(v) : "memory");
+  } else if constexpr (POL == 1) {
+    __builtin_nontemporal_store(v, a);
+  } else {
+    *a = v;
+  }
 }
 
 __device__ __forceinline__ void store16(uint8_t* p, int64_t col, const u32x4& v, int nt) {
@@ -284,13 +297,11 @@ __device__ __forceinline__ void mac3(Xacc& x, const kconst_u32* __restrict__ t, 
   x.add(__builtin_amdgcn_perm(t[4], t[4], s.s2));
 }
 
-// R output columns from the K source columns of one lane, then R stores.
-// SLICES = 3: production 3-bit-slice tables (ptab); 2: the round-1 2-bit
+// R output columns from the K source columns of one lane (combine_store:
+// then R stores).  SLICES = 3: production 3-bit-slice tables (ptab); 2: the round-1 2-bit
 // form (qtab), kept for A/B timing in the diagnostic library.
-template <int K, int R, int UNITS, int SLICES, int NTS>
-__device__ __forceinline__ void combine_store(const ApplyArgs& a, const u32x4 (&x)[K], uint8_t* const (&dp)[R],
-                                              int64_t col) {
-  u32x4 acc[R];
+template <int K, int R, int UNITS, int SLICES>
+__device__ __forceinline__ void combine(const ApplyArgs& a, const u32x4 (&x)[K], u32x4 (&acc)[R]) {
   if constexpr (SLICES == 3) {
     Xacc xa[R][4];
 #pragma unroll
@@ -333,14 +344,21 @@ __device__ __forceinline__ void combine_store(const ApplyArgs& a, const u32x4 (&
       }
     }
   }
+}
+
+template <int K, int R, int UNITS, int SLICES, int NTS>
+__device__ __forceinline__ void combine_store(const ApplyArgs& a, const u32x4 (&x)[K], uint8_t* const (&dp)[R],
+                                              int64_t col) {
+  u32x4 acc[R];
+  combine<K, R, UNITS, SLICES>(a, x, acc);
 #pragma unroll
   for (int r = 0; r < R; ++r) store16t<NTS>(dp[r], col, acc[r]);
 }
 
 // Lane l of block b handles the 16-byte columns (b*VEC + v)*256 + l, v < VEC,
 // of every shard of stripe s: all K*VEC loads are issued before any
-// arithmetic, then R*VEC stores.  NT: bit 0 = non-temporal loads, bit 1 =
-// non-temporal stores (VEC == 1; the VEC > 1 probe form follows a.nt).
+// arithmetic, then R*VEC stores.  NT: bit 0 = non-temporal loads, NT >> 1 =
+// store policy of store16t (VEC == 1; the VEC > 1 probe form follows a.nt).
 template <int K, int R, int UNITS, int VEC, int SLICES = 3, int NT = 3>
 __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
   const unsigned cblk = a.stripe_fast ? blockIdx.y : blockIdx.x;
@@ -361,7 +379,7 @@ __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
     u32x4 x[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) x[j] = load16t<NT & 1>(sp[j], col0);
-    combine_store<K, R, UNITS, SLICES, (NT >> 1) & 1>(a, x, dp, col0);
+    combine_store<K, R, UNITS, SLICES, (NT >> 1)>(a, x, dp, col0);
     return;
   }
 
@@ -417,9 +435,10 @@ __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
   }
 }
 
-// Production cache policy (A/B on MI355X): non-temporal loads
-// and stores (NT = 3).  The runtime can select plain stores per launch
-// (gf_spec.hpp store_nt) for tuning.
+// Cache policy: NT bit 0 = non-temporal loads, NT >> 1 = store policy
+// (store16t: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1).  The production
+// instantiations (gf_spec.hip) all load `nt` and select the store policy per
+// launch.
 template <int K, int R, int UNITS, int VEC = 1, int SLICES = 3, int NT = 3>
 __global__ __launch_bounds__(kBlock) void gf_apply(ApplyArgs a) {
   gf_apply_body<K, R, UNITS, VEC, SLICES, NT>(a);
@@ -455,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_dma(ApplyArgs a) {
   u32x4 x[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) x[j] = stage[w][j][lane];
-  combine_store<K, R, UNITS, SLICES, (NT >> 1) & 1>(a, x, dp, col);
+  combine_store<K, R, UNITS, SLICES, (NT >> 1)>(a, x, dp, col);
 }
 
 // Same body, register budget capped for 8 waves/SIMD (<= 64 VGPRs).
@@ -535,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm_stream(ApplyArgs a) {
 }
 
 // DIAGNOSTIC: streaming copy of shard 0 -> dst 0 (the HBM ceiling reference).
-// NT: bit 0 = non-temporal loads, bit 1 = non-temporal stores.
+// NT: bit 0 = non-temporal loads, NT >> 1 = store policy (store16t).
 template <int VEC, int NT = 1>
 __global__ __launch_bounds__(kBlock) void diag_copy(ApplyArgs a) {
   const int64_t col0 = int64_t(blockIdx.x) * (VEC * kBlock) + threadIdx.x;
@@ -548,7 +567,7 @@ __global__ __launch_bounds__(kBlock) void diag_copy(ApplyArgs a) {
     if (col0 + v * kBlock < a.nvec) x[v] = load16t<NT & 1>(sp, col0 + v * kBlock);
 #pragma unroll
   for (int v = 0; v < VEC; ++v)
-    if (col0 + v * kBlock < a.nvec) store16t<(NT >> 1) & 1>(dp, col0 + v * kBlock, x[v]);
+    if (col0 + v * kBlock < a.nvec) store16t<(NT >> 1)>(dp, col0 + v * kBlock, x[v]);
 }
 
 // ----------------------------------------------------------------- LDS ----

@@ -9,22 +9,24 @@
 namespace ecgpu {
 
 using SpecKernelFn = void (*)(dev::ApplyArgs);
+constexpr int kStorePolicies = 4;
 
-// Store cache policy of the production kernel: 0 plain, 1 non-temporal.
-// (Loads are always non-temporal.)  kind: ECGPU_KERNEL_PERM / _LDS.
+// store_pol: store cache policy of the production kernel, 0 plain, 1 nt,
+// 2 sc1, 3 sc0 sc1 (gf_kernels.hpp store16t; loads are always
+// non-temporal).  lds: the LDS nibble-table kernel instead.
 // unit_variant indexes kUnitVariants (ecgpu_runtime.hip).  nullptr if K is
 // outside 1..kMaxSpecK.
-SpecKernelFn spec_kernel_r1(bool lds, int K, int unit_variant, int store_nt);
-SpecKernelFn spec_kernel_r2(bool lds, int K, int unit_variant, int store_nt);
-SpecKernelFn spec_kernel_r3(bool lds, int K, int unit_variant, int store_nt);
-SpecKernelFn spec_kernel_r4(bool lds, int K, int unit_variant, int store_nt);
+SpecKernelFn spec_kernel_r1(bool lds, int K, int unit_variant, int store_pol);
+SpecKernelFn spec_kernel_r2(bool lds, int K, int unit_variant, int store_pol);
+SpecKernelFn spec_kernel_r3(bool lds, int K, int unit_variant, int store_pol);
+SpecKernelFn spec_kernel_r4(bool lds, int K, int unit_variant, int store_pol);
 
-inline SpecKernelFn spec_kernel(bool lds, int K, int R, int unit_variant, int store_nt) {
+inline SpecKernelFn spec_kernel(bool lds, int K, int R, int unit_variant, int store_pol) {
   switch (R) {
-    case 1: return spec_kernel_r1(lds, K, unit_variant, store_nt);
-    case 2: return spec_kernel_r2(lds, K, unit_variant, store_nt);
-    case 3: return spec_kernel_r3(lds, K, unit_variant, store_nt);
-    case 4: return spec_kernel_r4(lds, K, unit_variant, store_nt);
+    case 1: return spec_kernel_r1(lds, K, unit_variant, store_pol);
+    case 2: return spec_kernel_r2(lds, K, unit_variant, store_pol);
+    case 3: return spec_kernel_r3(lds, K, unit_variant, store_pol);
+    case 4: return spec_kernel_r4(lds, K, unit_variant, store_pol);
     default: return nullptr;
   }
 }

@@ -159,8 +159,9 @@ ECGPU_API ecgpu_plan* ecgpu_plan_create(int rows, int nsrc, const int* coefs, in
 ECGPU_API int ecgpu_plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src_ptrs, uint8_t* const* dst_ptrs,
                               int64_t size);
 /* kind: ECGPU_KERNEL_PERM (production) or ECGPU_KERNEL_LDS; nontemporal: store
- * cache policy of the production kernel (1 = non-temporal, the default; its
- * loads are always non-temporal). */
+ * cache policy of the production kernel: 0 plain, 1 non-temporal (the
+ * default), 2 sc1, 3 sc0 sc1 (written through, not kept in L2); its loads are
+ * always non-temporal. */
 ECGPU_API int ecgpu_plan_set_kernel(ecgpu_plan* p, int kind, int nontemporal);
 ECGPU_API int ecgpu_plan_launch(ecgpu_plan* p, void* stream);
 ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p);

@@ -199,6 +199,15 @@ def run_layout(args, k, m, S, B, pad):
                          14 * S * B, 1))
         variants.append((f"Y dec1dense {tag}", 13, 10, 1, ntb, 0, qdd, ndd, src_dec, dst_dec, B, udd, zdd,
                          11 * S * B, 1))
+    # explicit cache bits (diag variant 15, inline-asm loads / stores)
+    lnames = ["nt", "sc1nt", "sc0sc1nt", "sc0sc1", "sc1"]
+    snames = ["nt", "sc1", "sc0sc1", "sc0sc1nt", "sc1nt"]
+    for lp in range(5):
+        for sp in range(5):
+            variants.append((f"C enc L{lnames[lp]} S{snames[sp]}", 15, 10, 4, lp, sp, q_enc, n_enc, src_enc, dst_enc,
+                             B, u_enc, z_enc, (k + m) * S * B, 1))
+            variants.append((f"C dec1 L{lnames[lp]} S{snames[sp]}", 15, 10, 1, lp, sp, qd1, nd1, src_dec, dst_dec, B,
+                             ud1, zd1, (k + 1) * S * B, 1))
     variants = [v for v in variants if any(o in v[0] for o in only)]
     times = {v[0]: [] for v in variants}
     import random

@@ -11,10 +11,10 @@ Python mirrors the reference API by module (``galois``, ``reed_sol``,
 ``jerasure``) and adds the batched device-resident ``plan`` API.
 """
 from . import _native  # noqa: F401  -- fails loudly if the HIP extension is missing
-from . import ecx, galois, jerasure, pipeline, plan, reed_sol  # noqa: F401
+from . import ecx, formats, galois, jerasure, pipeline, plan, reed_sol  # noqa: F401
 from .pipeline import HostPipeline, HostPipelineGroup  # noqa: F401
 from .ecx import ParityAccumulator  # noqa: F401
 from .plan import DecodePlan, StripePlan, alloc_stripes, encode_plan  # noqa: F401
 
-__all__ = ["galois", "jerasure", "reed_sol", "plan", "StripePlan", "DecodePlan", "encode_plan", "alloc_stripes", "ecx",
+__all__ = ["galois", "jerasure", "reed_sol", "formats", "plan", "StripePlan", "DecodePlan", "encode_plan", "alloc_stripes", "ecx",
            "ParityAccumulator", "pipeline", "HostPipeline", "HostPipelineGroup"]

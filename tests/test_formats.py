@@ -1,0 +1,274 @@
+"""Wire / disk formats and the localhost cluster replay.
+
+CPU: ``erasure_coding_test_amd.formats`` against tests/golden/wire.json (gcc's
+layout of the reference's own ``metadata_t`` and byte images built the way the
+reference's senders build them, tests/golden/make_wire_golden.py), the
+reference's file-name / sidecar / padding / tail / block-split arithmetic, and
+the replay harness (tests/cluster_replay.py) driven with the checker as coder.
+GPU: the same replays with the product (GPU) coder, every chunk file and the
+read-back file compared byte for byte with the checker's.
+"""
+import itertools
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_DIR
+from ecdata import splitmix_bytes
+from erasure_coding_test_amd import formats as F
+
+_PORTS = itertools.count(0)
+
+
+@pytest.fixture(scope="module")
+def wire():
+    with open(os.path.join(GOLDEN_DIR, "wire.json")) as f:
+        return json.load(f)
+
+
+def test_metadata_layout_matches_reference(wire):
+    assert F.METADATA_SIZE == wire["sizeof"] == 312
+    for name, off in wire["offsets"].items():
+        assert getattr(F.MetadataT, name).offset == off, name
+    assert (F.EC_K, F.EC_M, F.EC_N, F.EC_W, F.EC_X, F.MAX_PATH_LEN) == (
+        wire["EC_K"], wire["EC_M"], wire["EC_N"], wire["EC_W"], wire["EC_X"], wire["MAX_PATH_LEN"])
+
+
+def test_metadata_images_match_reference(wire):
+    chunk = F.pack_metadata(sockfd=7, chunk_size=1048576, block_size=-1, data=0x7f00deadbeef0,
+                            dst_filename_datanode="/data/test_file/write/dst1_5")
+    assert chunk.hex() == wire["chunk_image"]
+    block = F.pack_metadata(sockfd=9, chunk_size=1048576, block_size=349525, remain_block_size=1, cur_block=2,
+                            cur_eck=1, error_flag=F.EC_ERROR, dst_filename_datanode="x/test_file/write/f1_2",
+                            net_block_size=[349525, 349526, 349527])
+    assert block.hex() == wire["block_image"]
+    md = F.unpack_metadata(bytes.fromhex(wire["block_image"]))
+    assert (md["sockfd"], md["chunk_size"], md["block_size"], md["remain_block_size"], md["cur_block"],
+            md["cur_eck"], md["error_flag"], md["net_block_size"]) == (9, 1048576, 349525, 1, 2, 1, -1,
+                                                                       [349525, 349526, 349527])
+    assert md["dst_filename_datanode"] == "x/test_file/write/f1_2"
+    assert F.unpack_metadata(bytes.fromhex(wire["chunk_image"]))["data"] == 0x7f00deadbeef0
+
+
+def test_metadata_variants_and_errors():
+    plain = F.metadata_struct(net_block_size=False)
+    assert F.ctypes.sizeof(plain) == 304  # error_flag at 296 + 4, padded to 8
+    assert F.ctypes.sizeof(F.metadata_struct(ec_x=4)) == 320
+    with pytest.raises(ValueError):
+        F.pack_metadata(dst_filename_datanode="x" * 256)
+    with pytest.raises(ValueError):
+        F.pack_metadata(net_block_size=[1, 2])
+    with pytest.raises(ValueError):
+        F.unpack_metadata(b"\0" * 311)
+
+
+def test_file_size_sidecar(wire):
+    assert F.file_size_sidecar(3145728).hex() == wire["sidecar_3145728"]
+    for n in (0, 1, 3145728, 2 ** 31 - 1, -5):
+        assert F.parse_file_size_sidecar(F.file_size_sidecar(n)) == n
+    with pytest.raises(ValueError):
+        F.parse_file_size_sidecar(b"123")
+    with pytest.raises(ValueError):
+        F.file_size_sidecar(2 ** 31)
+    raw = bytearray(256)
+    raw[:6] = b"  42ab"
+    assert F.parse_file_size_sidecar(bytes(raw)) == 42  # atoi: leading blanks, stops at a non-digit
+
+
+def test_names():
+    s = F.stripe_filename("/w/test_file/write/dst", 1)
+    assert s == "/w/test_file/write/dst1"
+    assert [F.chunk_filename(s, i) for i in (0, 5)] == ["/w/test_file/write/dst1_1", "/w/test_file/write/dst1_6"]
+    assert F.datanode_ip(0) == "192.168.7.102" and F.datanode_ip(-1) == "192.168.7.101"
+    assert F.replace_filename_suffix("a_b/dst1_2", 7) == "a_b/dst1_7"
+    with pytest.raises(ValueError):
+        F.replace_filename_suffix("nounderscore", 1)
+
+
+def test_read_padding(tmp_path):
+    p = tmp_path / "f"
+    p.write_bytes(b"abc")
+    buf = bytearray(8)
+    with open(p, "rb") as f:
+        assert F.read_file_to_buffer(f, buf) == 0
+    assert bytes(buf) == b"abc00000"  # '0' = 0x30, client_main.cpp:49
+    p.write_bytes(b"12345678")
+    with open(p, "rb") as f:
+        assert F.read_file_to_buffer(f, buf) == 1
+
+
+@pytest.mark.parametrize("file_size,expect", [(0, (0, (3, 0))), (1, (1, (0, 1))), (3 << 20, (1, (3, 0))),
+                                              ((3 << 20) + 5, (2, (0, 5))), ((2 << 20) + 7, (1, (2, 7)))])
+def test_stripes_and_tail(file_size, expect):
+    assert (F.stripe_count(file_size, 3, 1 << 20), F.read_tail(file_size, 3, 1 << 20)) == expect
+
+
+def test_last_stripe_bytes():
+    chunks = [b"AAAA", b"BBBB", b"CCCC"]
+    assert F.last_stripe_bytes(chunks, 1, 2) == b"AAAABB"
+    assert F.last_stripe_bytes(chunks, 3, 0) == b"AAAABBBBCCCC"
+
+
+@pytest.mark.parametrize("chunk,w,n", [(1 << 20, 8, 3), (1 << 20, 16, 3), (1 << 20, 32, 5), (1000, 8, 7), (7, 16, 3)])
+def test_eck_blocks_tile_the_chunk(chunk, w, n):
+    bs, rem = F.eck_block_sizes(chunk, w, n)
+    blocks = F.eck_blocks(chunk, w, n)
+    assert len(blocks) == n and blocks[0] == (0, bs + rem)
+    end = 0
+    for j, (off, size) in enumerate(blocks):
+        assert off == end and off == F.block_offset(j, bs, rem) == F.block_offset(j, bs, rem, [bs] * 3)
+        end += size
+    wb = w // 8
+    assert end == (chunk // wb) * wb  # trailing bytes of a chunk that is not whole words are never sent
+    assert (bs, rem) == (((chunk // wb) // n) * wb, ((chunk // wb) % n) * wb)
+
+
+def test_block_offset_isomerism():
+    # ENCODE_ISOMERISM: offsets from net_block_size[] (eck_datanode_main.cpp:451-471)
+    nbs = [80, 40, 10]
+    assert F.block_offset(0, 999, 3, nbs) == 0
+    assert F.block_offset(1, 999, 3, nbs) == 3 + 80
+    assert F.block_offset(3, 999, 3, nbs) == 3 + 130
+    assert F.block_offset(5, 999, 3, nbs) == 3 + 130 + 120
+
+
+def test_ecx_routing():
+    assert [F.ecx_node_for_block(j) for j in range(6)] == [3, 4, 5, 3, 4, 5]
+    assert F.ecx_blocks(3) == [0] and F.ecx_blocks(4, n=8) == [1, 4, 7]
+    for k, n, x in ((3, 3, 3), (10, 7, 3), (4, 9, 2)):
+        got = sorted(j for e in range(k, k + x) for j in F.ecx_blocks(e, k, n, x))
+        assert got == list(range(n))
+
+
+# ---- cluster replay ---------------------------------------------------------------
+
+def _layout(**kw):
+    from cluster_replay import Layout
+    # the reference's ports (8000-8100) shifted per test, kept below the ephemeral range (32768+):
+    # a listener may not bind a port an outgoing connection of this host holds
+    return Layout(port_offset=10000 + next(_PORTS) % 140 * 100, **kw)
+
+
+def _write_src(client, name, size, seed):
+    with open(client.src_path(name), "wb") as f:
+        f.write(splitmix_bytes(size, seed).tobytes())
+
+
+def _expected_chunks(coder, L, payload: bytes, stripe_no: int):
+    """The stripe's k data + m coding chunks, as the checker encodes them."""
+    buf = bytearray(L.k * L.chunk_size)
+    buf[:len(payload)] = payload
+    buf[len(payload):] = F.PAD_BYTE * (len(buf) - len(payload))
+    data = [np.frombuffer(buf, np.uint8, L.chunk_size, i * L.chunk_size).copy() for i in range(L.k)]
+    coding = [np.zeros(L.chunk_size, np.uint8) for _ in range(L.m)]
+    coder.encode(L.k, L.m, L.w, coder.coding_matrix(L.k, L.m, L.w), data, coding, L.chunk_size)
+    return [d.tobytes() for d in data + coding]
+
+
+def _check_chunks(cl, dst, expected_per_stripe):
+    for s, chunks in enumerate(expected_per_stripe, start=1):
+        name = F.stripe_filename(F.WRITE_PATH + dst, s)
+        for i, want in enumerate(chunks):
+            with open(cl.chunk_file(i, F.chunk_filename(name, i)), "rb") as f:
+                assert f.read() == want, (s, i)
+
+
+def _replay_write_read(tmp_path, coder, checker, L, file_size, kills, single=True, eck=False):
+    from cluster_replay import Cluster
+    with Cluster(str(tmp_path), coder, L) as cl:
+        c = cl.client()
+        _write_src(c, "src", file_size, 0xEC5EED ^ file_size)
+        raw = open(c.src_path("src"), "rb").read()
+        rc = c.write_eck("src", "dst") if eck else c.write("src", "dst", single_stripe_only=single)
+        assert rc == F.EC_OK
+        cl.check()
+        stripe = L.k * L.chunk_size
+        exp = [_expected_chunks(checker, L, raw[i:i + stripe], n + 1)
+               for n, i in enumerate(range(0, max(len(raw), 1), stripe))]
+        _check_chunks(cl, "dst", exp)
+        for idx in kills:
+            cl.kill(idx)
+        assert c.read("back", "dst") == F.EC_OK
+        cl.check()
+        back = open(os.path.join(c.base, F.READ_PATH, "back"), "rb").read()
+        assert back == raw
+        with open(os.path.join(c.base, F.FILE_SIZE_PATH + "dst"), "rb") as f:
+            assert f.read() == F.file_size_sidecar(file_size)
+
+
+@pytest.fixture(scope="module")
+def checker_coder(restatement):
+    from cluster_replay import OracleCoder
+    return OracleCoder(restatement)
+
+
+@pytest.mark.parametrize("kills", [(), (0,), (1, 2), (0, 1, 2)])
+def test_replay_write_read_checker(tmp_path, checker_coder, kills):
+    L = _layout(chunk_size=65536 + 5)
+    _replay_write_read(tmp_path, checker_coder, checker_coder, L, 3 * L.chunk_size, kills)
+
+
+def test_replay_write_rejects_non_stripe_files(tmp_path, checker_coder):
+    from cluster_replay import Cluster
+    L = _layout(chunk_size=4096)
+    with Cluster(str(tmp_path), checker_coder, L) as cl:
+        c = cl.client()
+        _write_src(c, "short", 3 * 4096 - 1, 1)
+        _write_src(c, "long", 3 * 4096 + 1, 2)
+        assert c.write("short", "d1") == F.EC_ERROR  # padded read (client_main.cpp:1710-1715)
+        assert c.write("long", "d2") == F.EC_ERROR  # reading != 1 (:1690-1695)
+
+
+@pytest.mark.parametrize("file_size", [1, 4096 * 3 * 2 + 17, 4096 * 5])
+def test_replay_multistripe_tail_checker(tmp_path, checker_coder, file_size):
+    L = _layout(chunk_size=4096)
+    _replay_write_read(tmp_path, checker_coder, checker_coder, L, file_size, (1,), single=False)
+
+
+def test_replay_too_many_dead_nodes(tmp_path, checker_coder):
+    from cluster_replay import Cluster
+    L = _layout(k=4, m=2, chunk_size=4096, ec_x=2, ec_n=2)
+    with Cluster(str(tmp_path), checker_coder, L) as cl:
+        c = cl.client()
+        _write_src(c, "src", 4 * 4096, 3)
+        assert c.write("src", "dst") == F.EC_OK
+        for idx in (0, 1, 3):
+            cl.kill(idx)
+        assert c.read("back", "dst") == F.EC_ERROR  # num_need_coding > EC_M (:2086-2091)
+
+
+@pytest.mark.parametrize("k,m,x,n,chunk", [(3, 3, 3, 3, 1 << 16), (4, 2, 2, 5, 10007), (5, 3, 2, 4, 4096)])
+def test_replay_eck_ecx_checker(tmp_path, checker_coder, k, m, x, n, chunk):
+    L = _layout(k=k, m=m, ec_x=x, ec_n=n, chunk_size=chunk)
+    _replay_write_read(tmp_path, checker_coder, checker_coder, L, k * chunk - 3, (0,), eck=True)
+
+
+# ---- GPU: the product coder in the same replays ---------------------------------------
+
+@pytest.fixture(scope="module")
+def product_coder(gpu):
+    from cluster_replay import ProductCoder
+    return ProductCoder()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kills", [(), (2,), (0, 1, 2)])
+def test_replay_write_read_gpu(tmp_path, product_coder, checker_coder, kills):
+    L = _layout(chunk_size=(1 << 20) + 3)  # the reference's 1 MiB chunks, ragged by 3 bytes
+    _replay_write_read(tmp_path, product_coder, checker_coder, L, 3 * L.chunk_size, kills)
+
+
+@pytest.mark.gpu
+def test_replay_multistripe_gpu(tmp_path, product_coder, checker_coder):
+    L = _layout(k=10, m=4, ec_x=4, ec_n=4, chunk_size=65536)
+    _replay_write_read(tmp_path, product_coder, checker_coder, L, 10 * 65536 * 3 + 12345, (0, 5, 9, 3), single=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,x,n,chunk", [(3, 3, 3, 3, 1 << 20), (10, 4, 4, 8, 349525 * 3 + 1)])
+def test_replay_eck_ecx_gpu(tmp_path, product_coder, checker_coder, k, m, x, n, chunk):
+    """ECX incremental encode on the GPU accumulators (ParityAccumulator) vs the checker."""
+    L = _layout(k=k, m=m, ec_x=x, ec_n=n, chunk_size=chunk)
+    _replay_write_read(tmp_path, product_coder, checker_coder, L, k * chunk, (1,), eck=True)

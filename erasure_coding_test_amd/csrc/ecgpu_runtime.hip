@@ -7,7 +7,7 @@
 //     streaming launch per <= 4 output rows;
 //   * buffers are classified per pointer: device memory is used in place,
 //     host memory is staged through a per-context HBM slab with
-//     hipMemcpyAsync on that context's own non-blocking stream;
+//     hipMemcpyAsync on that context's own stream (ordered after the null stream);
 //   * contexts (stream + staging + plan cache) come from a process-wide
 //     pool, so concurrent callers (the reference's encode pthreads,
 //     client_main.cpp:1074-1164) never share a stream or a lock on the
@@ -187,6 +187,17 @@ void build_wide_tables(uint32_t c, int W, uint32_t* t) {
   }
 }
 
+// LDS nibble tables of gf_apply_wide_nib: T_t[v] = c*(v << 4t) at w = 32; at
+// w = 16 tables 0..3 serve the low word of a dword and 4..7 the high word
+// (entries shifted into bits 16..31).
+void build_wide_nib_tables(uint32_t c, int w, uint32_t* t) {
+  for (int tt = 0; tt < 8; ++tt)
+    for (uint32_t v = 0; v < 16; ++v)
+      t[tt * 16 + int(v)] = w == 32  ? gf_mul_poly(v << (4 * tt), c, 32)
+                            : tt < 4 ? gf_mul_poly(v << (4 * tt), c, 16)
+                                     : gf_mul_poly(v << (4 * (tt - 4)), c, 16) << 16;
+}
+
 int wide_words_per_coef(int w) { return w == 16 ? 2 * dev::Wide<2>::kPerms : 2 * dev::Wide<4>::kPerms; }
 
 }  // namespace
@@ -201,6 +212,7 @@ struct ecgpu_plan {
   uint8_t* d_nib = nullptr;
   uint32_t* d_w = nullptr;     // wide-word tables (w = 16 / 32)
   uint8_t* d_wcls = nullptr;   // wide coefficient classes
+  uint32_t* d_wnib = nullptr;  // wide-word LDS nibble tables, kNibWords per coefficient
   int stripes = 0;
   int64_t size = 0;
   bool aligned = true;
@@ -231,6 +243,7 @@ void plan_free(ecgpu_plan* p) {
   if (p->d_nib) (void)hipFree(p->d_nib);
   if (p->d_w) (void)hipFree(p->d_w);
   if (p->d_wcls) (void)hipFree(p->d_wcls);
+  if (p->d_wnib) (void)hipFree(p->d_wnib);
   if (p->d_src) (void)hipFree(p->d_src);
   if (p->d_dst) (void)hipFree(p->d_dst);
   delete p;
@@ -250,16 +263,20 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
     const int nw = wide_words_per_coef(w);
     std::vector<uint32_t> t(n * size_t(nw));
     std::vector<uint8_t> cls(n);
+    std::vector<uint32_t> nib(n * size_t(dev::kNibWords));
     for (size_t i = 0; i < n; ++i) {
       p->coef[i] = uint32_t(coefs[i]) & mask;
       cls[i] = p->coef[i] == 0 ? 2 : p->coef[i] == 1 ? 1 : 0;
       build_wide_tables(p->coef[i], w / 8, &t[i * size_t(nw)]);
+      build_wide_nib_tables(p->coef[i], w, &nib[i * size_t(dev::kNibWords)]);
     }
     DeviceGuard g(device);
     ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_w), t.size() * sizeof(uint32_t)));
     ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_wcls), n));
+    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_wnib), nib.size() * sizeof(uint32_t)));
     ECGPU_HIP(hipMemcpy(p->d_w, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     ECGPU_HIP(hipMemcpy(p->d_wcls, cls.data(), n, hipMemcpyHostToDevice));
+    ECGPU_HIP(hipMemcpy(p->d_wnib, nib.data(), nib.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     return ECGPU_OK;
   }
   for (size_t i = 0; i < n; ++i) p->coef[i] = uint32_t(coefs[i]) & 0xFFu;
@@ -314,26 +331,68 @@ int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* co
 }
 
 // w = 16 / 32: 16-B column kernel over the aligned part, word kernel for the
-// rest; size must be a whole number of words (checked by the callers).
+// rest; size must be a whole number of words (checked by the callers).  The
+// column kernel is gf_apply_wide_nib (LDS nibble tables) when a launch's
+// tables fit in kNibMaxLds, else gf_apply_wide (v_perm); ECGPU_WIDE=1 forces
+// v_perm (A/B, tools/bench_surface.py).
+int multiprocessors(int device) {
+  static std::once_flag once;
+  static int n = 0;
+  std::call_once(once, [&] {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) n = 256;
+  });
+  return n;
+}
+
+// Resident workgroups per CU of a kernel at kBlock threads and `lds` bytes
+// of dynamic LDS (cached; the launch shapes are few).
+int resident_blocks(KernelFn fn, unsigned lds) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<const void*, unsigned>, int>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(reinterpret_cast<const void*>(fn), lds);
+  for (const auto& e : cache)
+    if (e.first == key) return e.second;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), dev::kBlock, lds) !=
+          hipSuccess ||
+      n <= 0)
+    n = 4;
+  cache.emplace_back(key, n);
+  return n;
+}
+
 int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
   const int K = p->nsrc, W = p->w / 8, nw = wide_words_per_coef(p->w);
   const int64_t nvec = p->aligned ? p->size / 16 : 0;
   const int64_t byte0 = nvec * 16;
   const dim3 block(dev::kBlock);
   constexpr int kMaxGridY = 65535;
+  const bool force_perm = env_int("ECGPU_WIDE", 0) == 1;
   for (int r0 = 0; r0 < p->rows; r0 += dev::kMaxRows) {
     const int R = std::min(dev::kMaxRows, p->rows - r0);
+    const unsigned nib_lds = unsigned(K) * unsigned(dev::nib_source_bytes(R));
+    const bool nib = !force_perm && nib_lds <= unsigned(dev::kNibMaxLds);
     KernelFn vec_fn = nullptr, word_fn = W == 2 ? &dev::gf_apply_wide_words<2> : &dev::gf_apply_wide_words<4>;
-    switch (R) {
-      case 1: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 1> : &dev::gf_apply_wide<4, 1>; break;
-      case 2: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 2> : &dev::gf_apply_wide<4, 2>; break;
-      case 3: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 3> : &dev::gf_apply_wide<4, 3>; break;
-      default: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 4> : &dev::gf_apply_wide<4, 4>; break;
+    if (nib) {
+      switch (R) {
+        case 1: vec_fn = &dev::gf_apply_wide_nib<1>; break;
+        case 2: vec_fn = &dev::gf_apply_wide_nib<2>; break;
+        case 3: vec_fn = &dev::gf_apply_wide_nib<3>; break;
+        default: vec_fn = &dev::gf_apply_wide_nib<4>; break;
+      }
+    } else {
+      switch (R) {
+        case 1: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 1> : &dev::gf_apply_wide<4, 1>; break;
+        case 2: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 2> : &dev::gf_apply_wide<4, 2>; break;
+        case 3: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 3> : &dev::gf_apply_wide<4, 3>; break;
+        default: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 4> : &dev::gf_apply_wide<4, 4>; break;
+      }
     }
     for (int s0 = 0; s0 < p->stripes; s0 += kMaxGridY) {
       const int ns = std::min(kMaxGridY, p->stripes - s0);
       ApplyArgs a{};
-      a.wtab = p->d_w + size_t(r0) * K * nw;
+      a.wtab = nib ? p->d_wnib + size_t(r0) * K * dev::kNibWords : p->d_w + size_t(r0) * K * nw;
       a.wcls = p->d_wcls + size_t(r0) * K;
       a.src = p->d_src + size_t(s0) * K;
       a.dst = p->d_dst + size_t(s0) * p->rows;
@@ -347,11 +406,23 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
       a.R = R;
       a.nt = p->nt;
       if (nvec > 0) {
-        const dim3 grid(unsigned((nvec + dev::kBlock - 1) / dev::kBlock), unsigned(ns));
-        ECGPU_HIP(launch(vec_fn, grid, block, a, stream));
+        const int64_t nblk = (nvec + dev::kBlock - 1) / dev::kBlock;
+        if (nib) {
+          // exactly one resident round of workgroups (occupancy x CUs), each
+          // looping over column blocks: a second, partial round would run
+          // on part of the chip
+          const int64_t per_stripe =
+              std::max<int64_t>(1, int64_t(multiprocessors(p->device)) * resident_blocks(vec_fn, nib_lds) / ns);
+          const dim3 grid(unsigned(std::min(nblk, per_stripe)), unsigned(ns));
+          ECGPU_HIP(launch(vec_fn, grid, block, a, stream, nib_lds));
+        } else {
+          ECGPU_HIP(launch(vec_fn, dim3(unsigned(nblk), unsigned(ns)), block, a, stream));
+        }
       }
       const int64_t words = (p->size - byte0) / W;
       if (words > 0) {
+        // the word kernel reads the v_perm tables
+        a.wtab = p->d_w + size_t(r0) * K * nw;
         const dim3 grid(unsigned((words + dev::kBlock - 1) / dev::kBlock), unsigned(ns));
         ECGPU_HIP(launch(word_fn, grid, block, a, stream));
       }
@@ -464,7 +535,12 @@ Ctx* acquire_ctx(int device, int* rc) {
   auto* c = new Ctx();
   c->device = device;
   DeviceGuard g(device);
-  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  // A blocking stream: a synchronous call on device buffers is ordered after
+  // work the caller queued on the null stream (PyTorch's default stream,
+  // e.g. the fill of a freshly allocated output), and that stream's later
+  // work after the call.  Calls from different threads still run on
+  // different contexts, unordered against each other.
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamDefault);
   if (e != hipSuccess) {
     *rc = fail(ECGPU_ERR_HIP, std::string("hipStreamCreateWithFlags: ") + hipGetErrorString(e));
     delete c;
@@ -1311,6 +1387,13 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
   bool aligned = ps % 8 == 0 && spstride % 8 == 0 && dstride % 8 == 0;
   for (auto* p : sb) aligned &= (reinterpret_cast<uintptr_t>(p) & 7u) == 0;
   for (auto* p : db) aligned &= (reinterpret_cast<uintptr_t>(p) & 7u) == 0;
+  // 16-B lanes when everything is 16-B aligned; ECGPU_PACKET=1 forces 8-B
+  // lanes (A/B, RS(10,4) w = 8 64 MiB bit-matrix encode on MI355X: 16-B lanes
+  // with 8 source rows in flight 186 us, 4 in flight 198, 8-B lanes 190)
+  const int packet_kind = env_int("ECGPU_PACKET", 0);
+  bool wide16 = aligned && packet_kind != 1 && ps % 16 == 0 && spstride % 16 == 0 && dstride % 16 == 0;
+  for (auto* p : sb) wide16 &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  for (auto* p : db) wide16 &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
   for (int g0 = 0; g0 < ngroups; ++g0) {
     const int R = std::min(kPacketRows, rows - g0 * kPacketRows);
     dev::PacketArgs a{};
@@ -1321,7 +1404,7 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
     a.dstride = dstride;
     a.nsrc = nsrc;
     a.R = R;
-    a.cpp = aligned ? ps / 8 : ps;
+    a.cpp = wide16 ? ps / 16 : aligned ? ps / 8 : ps;
     a.ncols = nsp * a.cpp;
     if (nsrc == 0) {  // every output packet is zero
       for (int r = 0; r < R; ++r)
@@ -1329,10 +1412,16 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
                                    size_t(nsp), c->stream));
       continue;
     }
-    void* fn = aligned ? (R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets<8>)
-                          : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets<16>)
-                                    : reinterpret_cast<void*>(&dev::gf_xor_packets<32>))
-                       : reinterpret_cast<void*>(&dev::gf_xor_packets_bytes);
+    void* fn = nullptr;
+    if (wide16)
+      fn = R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets16<8, 8>)
+           : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets16<16, 8>)
+                     : reinterpret_cast<void*>(&dev::gf_xor_packets16<32, 8>);
+    else
+      fn = aligned ? (R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets<8>)
+                      : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets<16>)
+                                : reinterpret_cast<void*>(&dev::gf_xor_packets<32>))
+                   : reinterpret_cast<void*>(&dev::gf_xor_packets_bytes);
     void* args[] = {&a};
     const dim3 grid(unsigned((a.ncols + dev::kBlock - 1) / dev::kBlock));
     ECGPU_HIP(hipLaunchKernel(fn, grid, dim3(dev::kBlock), args, 0, c->stream));

@@ -893,6 +893,10 @@ __device__ __forceinline__ void xor_masked(uint32_t (&acc)[RT][2], const u32x2& 
     acc[r][0] = __builtin_amdgcn_bitop3_b32(acc[r][0], x.x, sel, 0x78);  // a ^ (b & c): 0xF0 ^ (0xCC & 0xAA)
     acc[r][1] = __builtin_amdgcn_bitop3_b32(acc[r][1], x.y, sel, 0x78);
   }
+  // keep each source's row selectors local: hoisted over several sources they
+  // exceed the SGPR file and spill to VGPR lanes (v_writelane / v_readlane,
+  // VALU work as large as the XORs themselves at RT = 32)
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int RT>
@@ -925,6 +929,48 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets(PacketArgs a) {
     if (r < a.R) *(gu32x2*)(dp[r] + doff) = u32x2{acc[r][0], acc[r][1]};
 }
 
+// 16-byte form (packet sizes, strides and bases 16-B aligned): lane g owns
+// 16 bytes of one packet column, so every SALU row-mask extract serves four
+// dwords instead of two and a wave moves 1 KiB per load; CHUNK source rows
+// are loaded before the first use.  Non-temporal loads and stores, as the
+// matrix kernels.
+template <int RT, int CHUNK>
+__device__ __forceinline__ void xor_masked16(uint32_t (&acc)[RT][4], const u32x4& x, uint32_t m) {
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const uint32_t sel = uint32_t(int32_t(m << (31 - r)) >> 31);  // 0 or ~0, wave-uniform (SALU)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = __builtin_amdgcn_bitop3_b32(acc[r][c], x[c], sel, 0x78);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // selectors stay per source (see xor_masked)
+}
+
+template <int RT, int CHUNK>
+__global__ __launch_bounds__(kBlock) void gf_xor_packets16(PacketArgs a) {
+  const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= a.ncols) return;
+  int64_t sp, col;
+  packet_coords(a, g, &sp, &col);
+  const int64_t soff = sp * a.sstride + col * 16, doff = sp * a.dstride + col * 16;
+  uint32_t acc[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+  int j = 0;
+  for (; j + CHUNK <= a.nsrc; j += CHUNK) {
+    u32x4 x[CHUNK];
+#pragma unroll
+    for (int u = 0; u < CHUNK; ++u) x[u] = load16t<1>(a.src[j + u] + soff, 0);
+#pragma unroll
+    for (int u = 0; u < CHUNK; ++u) xor_masked16<RT, CHUNK>(acc, x[u], a.mask[j + u]);
+  }
+  for (; j < a.nsrc; ++j) xor_masked16<RT, CHUNK>(acc, load16t<1>(a.src[j] + soff, 0), a.mask[j]);
+  // output pointers only now: held across the loop they would take RT SGPR
+  // pairs from the row selectors (no store precedes these scalar loads)
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+    if (r < a.R) store16t<1>(a.dst[r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+}
+
 // Byte form for packet sizes / bases that are not 8-byte aligned.
 static __global__ __launch_bounds__(kBlock) void gf_xor_packets_bytes(PacketArgs a) {
   const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
@@ -941,6 +987,114 @@ static __global__ __launch_bounds__(kBlock) void gf_xor_packets_bytes(PacketArgs
       if ((m >> r) & 1u) out[r] ^= x;
   }
   for (int r = 0; r < a.R; ++r) a.dst[r][doff] = out[r];
+}
+
+// ------------------------------------- wide words, LDS nibble tables ----
+// Second engine for w = 16 / 32 (production when the tables fit, below).
+// c*x is GF(2)-linear, so for any dword x of a w = 16 / 32 region
+//     c*x = XOR_t T_t[nibble t of x],   t = 0..7,
+// with eight 16-entry dword tables per coefficient: w = 32: T_t[v] =
+// c*(v << 4t); w = 16 (two words per dword): T_t[v] = c*(v << 4t) for t < 4
+// (low word, entries in bits 0..15) and (c*(v << 4(t-4))) << 16 for t >= 4
+// (high word).  Unit and zero coefficients are the identity / zero tables,
+// so the body is branch-free.  The launch's rows share one LDS entry per
+// (source, t, v): 8 B for R <= 2 (ds_read_b64), 16 B for R = 3, 4
+// (ds_read_b128): one read does every row's lookup at the LDS array's full
+// 256 B/clk (MI355X_MICROARCH.md §LDS; two ds_read_b64 at a 1 KiB distance
+// would be merged by the compiler into ds_read2_b64, which runs at half that
+// rate), and a 16-entry table of 8- or 16-B entries never puts two distinct
+// addresses of one lane group on a bank.  Per source dword: 16 VALU for the
+// eight lookup addresses (shared by every row), 8 LDS reads and 4 XOR3 per
+// row -- against 32 v_perm per coefficient at w = 32 for gf_apply_wide.
+// Workgroups loop over column blocks so the table staging (K * 1 or 2 KiB
+// from L2) is amortised.
+constexpr int kNibWords = 128;  // dwords of one coefficient's 8 tables
+constexpr int kNibMaxLds = 64 * 1024;
+
+__host__ __device__ constexpr int nib_entry_words(int R) { return R <= 2 ? 2 : 4; }
+// LDS bytes of one source's tables for a launch of R rows
+__host__ __device__ constexpr int nib_source_bytes(int R) { return kNibWords * 4 * nib_entry_words(R); }
+
+typedef __attribute__((address_space(3))) const u32x2 lds_u32x2;
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void gf_apply_wide_nib(ApplyArgs a) {
+  constexpr int EW = nib_entry_words(R), EB = 4 * EW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t nib_lds[];
+  const int K = a.K;
+  // LDS dword ((j * 128 + t * 16 + v) * EW + r) = T[r][j][t][v] (0 for r >= R);
+  // a.wtab is [R][K][kNibWords] for this launch's rows
+  const int n = K * kNibWords * EW;
+  for (int i = threadIdx.x; i < n; i += kBlock) {
+    const int r = i % EW, e = (i / EW) % kNibWords, j = i / (EW * kNibWords);
+    reinterpret_cast<uint32_t*>(nib_lds)[i] = r < R ? a.wtab[size_t(r * K + j) * kNibWords + e] : 0u;
+  }
+  __syncthreads();
+
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(static_cast<void*>(nib_lds)));
+  constexpr int kChunk = 8;  // source loads in flight before the first use
+  const int64_t nblk = (a.nvec + kBlock - 1) / kBlock;
+  for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const int64_t col = b * kBlock + threadIdx.x;
+    if (col >= a.nvec) continue;
+    u32x4 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+    for (int j0 = 0; j0 < K; j0 += kChunk) {
+      u32x4 xs[kChunk];
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u)
+        if (j0 + u < K) xs[u] = load16t<1>(sp[j0 + u], col);
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u) {
+        const int j = j0 + u;
+        if (j >= K) break;
+        // LDS byte address of source j's tables; the kernel has no static LDS,
+        // so the dynamic allocation starts at 0 and jbase < 64 KiB (K <= 32)
+        const uint32_t jbase = lds_base + uint32_t(j) * uint32_t(nib_source_bytes(R));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t x = xs[u][c];
+          // lookup addresses, one v_perm each: nibble t = 2b (+1) of x, scaled
+          // by EB, sits in byte b of ns[0] (ns[1]); v_perm takes that byte and
+          // bytes 1, 2 of jbase (< 64 KiB, byte 0 zero); t's table offset is
+          // the ds_read immediate
+          constexpr int kSh = EB == 16 ? 4 : 3;
+          constexpr uint32_t kNibMask = 0x0F0F0F0Fu << kSh;
+          const uint32_t ns[2] = {(x << kSh) & kNibMask, (x >> (4 - kSh)) & kNibMask};
+          uint32_t v[8][EW];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
+                                uint32_t(t * 16 * EB);
+            if constexpr (EW == 2) {
+              const u32x2 q = *(lds_u32x2*)(size_t(ad));
+              v[t][0] = q.x;
+              v[t][1] = q.y;
+            } else {
+              const u32x4 q = *(lds_u32x4*)(size_t(ad));
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[t][r] = q[r];
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            uint32_t e = xor3(acc[r][c], v[0][r], v[1][r]);
+#pragma unroll
+            for (int t = 2; t < 8; t += 2) e = xor3(e, v[t][r], v[t + 1][r]);
+            acc[r][c] = e;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
+  }
 }
 
 }  // namespace dev

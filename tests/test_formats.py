@@ -148,6 +148,10 @@ def _layout(**kw):
     from cluster_replay import Layout
     # the reference's ports (8000-8100) shifted per test, kept below the ephemeral range (32768+):
     # a listener may not bind a port an outgoing connection of this host holds
+    # a pytest-xdist worker gets its own loopback /24, so parallel workers never share an address
+    worker = os.environ.get("PYTEST_XDIST_WORKER", "gw0")
+    wid = int(worker[2:]) if worker[2:].isdigit() else 0
+    kw.setdefault("prefix", f"127.0.{7 + wid % 200}.")
     return Layout(port_offset=10000 + next(_PORTS) % 140 * 100, **kw)
 
 

@@ -675,6 +675,39 @@ def test_wide_word_matrix_coding_device(ec, gpu, w, size, offset):
 
 
 @pytest.mark.parametrize("w", [16, 32])
+@pytest.mark.parametrize("engine", ["nib", "perm"])
+@pytest.mark.parametrize("k,m", [(3, 1), (5, 2), (7, 3), (9, 7), (33, 4), (40, 5)])
+def test_wide_word_random_matrix_engines(ec, gpu, monkeypatch, w, engine, k, m):
+    """Random w = 16 / 32 coding matrices (zeros, units and general
+    coefficients) through both column engines -- LDS nibble tables
+    (gf_apply_wide_nib; k = 33 / 40 with 4 rows exceed its LDS budget and
+    take v_perm) and v_perm (ECGPU_WIDE=1) -- against the reference library.
+    1..4 rows per launch and a second launch for m > 4."""
+    import torch
+    if engine == "perm":
+        monkeypatch.setenv("ECGPU_WIDE", "1")
+    else:
+        monkeypatch.delenv("ECGPU_WIDE", raising=False)
+    ref = _ref_nsa()
+    rng = np.random.default_rng(1000 * w + 10 * k + m)
+    hi = (1 << w) - 1
+    M = [int(x) for x in rng.integers(0, hi, k * m, dtype=np.uint64, endpoint=True)]
+    for i in rng.choice(k * m, size=(k * m) // 4, replace=False):
+        M[int(i)] = int(rng.integers(0, 2))  # zeros and units mixed in
+    size = (1 << 16) + 48 + (w // 8)  # whole 16-B columns + a word tail
+    data = [rng.integers(0, 256, size + 64, dtype=np.uint8) for _ in range(k)]
+    coding = [np.zeros(size + 64, np.uint8) for _ in range(m)]
+    ref._Z22jerasure_matrix_encodeiiiPiPPcS1_i(k, m, w, _cints([x if x < 2**31 else x - 2**32 for x in M]),
+                                              _cptrs(data), _cptrs(coding), size)
+    dd = [torch.from_numpy(a[:size].copy()).to(gpu) for a in data]
+    dc = [torch.full((size,), 0x5A, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, w, [x if x < 2**31 else x - 2**32 for x in M], dd, dc, size)
+    torch.cuda.synchronize()
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
+
+
+@pytest.mark.parametrize("w", [16, 32])
 def test_wide_word_region_ops_device(ec, gpu, w):
     import torch
     size = 8192 + 8

@@ -54,6 +54,11 @@ def main():
     for w in (8, 16, 32):
         M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w)
         rec(f"jerasure_matrix_encode w={w}", lambda M=M, w=w: J.jerasure_matrix_encode(k, m, w, M, data, coding, S))
+        if w != 8:  # A/B: the v_perm column engine (read per launch by the runtime)
+            os.environ["ECGPU_WIDE"] = "1"
+            rec(f"jerasure_matrix_encode w={w} (v_perm engine, ECGPU_WIDE=1)",
+                lambda M=M, w=w: J.jerasure_matrix_encode(k, m, w, M, data, coding, S))
+            del os.environ["ECGPU_WIDE"]
     M8 = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     bm = J.jerasure_matrix_to_bitmatrix(k, m, 8, M8)
     for ps in (1024, 4096, 65536):

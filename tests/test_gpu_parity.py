@@ -985,3 +985,50 @@ def test_random_decode_vs_reference(ec, gpu, reference, seed):
     assert rc_got == rc_ref, (k, m, erasures, row_k_ones)
     for i in range(k + m):
         assert np.array_equal(got_bufs[i], ref_bufs[i]), (k, m, erasures, row_k_ones, i)
+
+
+# ------------------------------------------------ size edge cases ----
+def test_empty_regions_touch_nothing(ec, gpu):
+    """size 0 (the reference's loops run zero times): outputs keep their bytes,
+    decode still reports success for a decodable pattern."""
+    import torch
+    k, m = 4, 2
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    dd = [torch.full((64,), 7 * i + 1, dtype=torch.uint8, device=gpu) for i in range(k)]
+    dc = [torch.full((64,), 0x5A, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, dd, dc, 0)
+    assert ec.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, [0, k], dd, dc, 0) == 0
+    torch.cuda.synchronize()
+    assert all(bool((c == 0x5A).all()) for c in dc)
+    assert all(bool((d == 7 * i + 1).all()) for i, d in enumerate(dd))
+
+
+@pytest.mark.parametrize("k,m,erasures", [(2, 1, [0]), (3, 2, [0, 2])])
+def test_maximum_int_size_roundtrip(ec, gpu, k, m, erasures):
+    """Shards of 2^31 - 1 bytes, the largest `int size` the reference API
+    takes (134M 16-B columns plus a 15-byte tail): encode -> erase -> decode
+    restores the data bit-exactly; for RS(k,1) the parity row is all ones, so
+    it must equal the XOR of the data (computed by torch, independent of the
+    library's kernels)."""
+    import torch
+    size = 2**31 - 1
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    g = torch.Generator(device=gpu).manual_seed(k * 10 + m)
+    dd = [torch.randint(0, 256, (size,), dtype=torch.uint8, device=gpu, generator=g) for _ in range(k)]
+    dc = [torch.empty(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, dd, dc, size)
+    torch.cuda.synchronize()
+    if m == 1:
+        x = dd[0].clone()
+        for d in dd[1:]:
+            x.bitwise_xor_(d)
+        assert torch.equal(x, dc[0])
+        del x
+    keep = {e: (dd + dc)[e].clone() for e in erasures}
+    for e in erasures:
+        (dd + dc)[e].fill_(0)
+    torch.cuda.synchronize()
+    assert ec.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, erasures, dd, dc, size) == 0
+    torch.cuda.synchronize()
+    for e, want in keep.items():
+        assert torch.equal((dd + dc)[e], want), e

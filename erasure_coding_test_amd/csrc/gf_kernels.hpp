@@ -8,20 +8,25 @@
 // no MFMA; 16-byte coalesced loads/stores; all K source columns of a lane
 // are loaded before any arithmetic so a wave has K*16 B per lane in flight.
 //
-// Two multiply engines:
-//  * PERM (default): c*x is GF(2)-linear in x, so split every byte into four
-//    2-bit slices, c*x = T0[x&3] ^ T1[(x>>2)&3] ^ T2[(x>>4)&3] ^ T3[x>>6] with
-//    Tp[e] = c*(e << 2p).  Each Tp is 4 bytes = ONE dword, so one v_perm_b32
-//    looks up 4 bytes at once with the table held in a (scalar) register:
-//    4 v_perm + 2 v_xor3 per coefficient per dword, tables fetched by
-//    s_load (wave-uniform), no LDS, no bank conflicts.  The 4 selector words
-//    are computed once per source dword and shared by all R rows.
-//  * LDS (the north-star layout): per coefficient the two 16-entry nibble
-//    tables T_lo[x] = c*x, T_hi[x] = c*(x<<4) are staged once per workgroup
-//    in LDS (32 B per coefficient; a 16-B table spans 4 banks, so lanes of
-//    one group never conflict) and every byte costs 2 ds_read_u8.
-// Coefficients 0 and 1 are detected from the (uniform) table word and take a
-// scalar branch: skip / plain XOR.
+// Multiply engines:
+//  * gf_apply<K,R,UNITS> (production, w = 8): c*x is GF(2)-linear in x, so a
+//    byte splits into bit slices [0:2], [3:5], [6:7] and
+//    c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6] with Tp[e] = c*(e << 3p); one
+//    v_perm_b32 looks up four bytes at once from tables held in scalar
+//    registers (3 v_perm per coefficient-dword), terms fold three at a time
+//    with v_bitop3 (XOR3), and unit coefficients are plain XORs from a
+//    compile-time structure the host checks per launch.  K and R are
+//    compile-time; gf_apply_perm_generic covers K > 16 and gf_apply_bytes
+//    shard tails and misaligned pointers.
+//  * gf_apply_lds<K,R> (w = 8, selectable): per coefficient the two
+//    16-entry nibble tables T_lo[x] = c*x, T_hi[x] = c*(x<<4) live in LDS and
+//    every byte costs 2 ds_read_u8 (LDS-issue-bound; also the bench's
+//    independent self-check engine).
+//  * gf_apply_wide_nib<R> / gf_apply_wide<W,R> (w = 16 / 32) and
+//    gf_xor_packets16 / gf_xor_packets (GF(2) bit-matrix / schedule coding):
+//    see their sections below.
+// gf_apply_perm (2-bit slices, runtime coefficient classes) and the LDS-DMA
+// form are kept for the A/B probes of the diagnostic library.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

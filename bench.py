@@ -350,7 +350,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "gf_apply (encode launch)", "algorithmic_bytes_per_launch": enc_bytes,
-                         "avg_launch_ms": round(enc_ms, 4)},
+                         "avg_launch_ms": round(enc_ms, 4),
+                         # the north star's read-only accounting: data-shard bytes only, which
+                         # caps at k/(k+m) = 0.714 of peak for any encode
+                         "read_only_frac": round(k * S * B / (enc_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
             "copy_ceiling": copy,
             "encode_frac_of_copy": round(achieved / copy["GBps"], 4) if copy else None,
             "decode_kernel": {"avg_launch_ms": round(dec_ms, 4), "algorithmic_bytes_per_launch": dec_bytes,

@@ -654,6 +654,60 @@ void add_stats(const FusedOp& op) {
   g_stats[2] += op.memcpy_bytes;
 }
 
+// Moves n shards of `bytes` between host pointers hp[i] and device shards
+// d0 + i * dstride.  Every run of >= 2 evenly spaced host shards (a stripe
+// laid out in one host slab, as the reference client's stripe buffer is,
+// client_main.cpp:1619-1647) goes as ONE 2-D copy, the rest one copy per
+// shard.  ECGPU_PIPE_2D=0 always copies per shard.  Used by the pipelines and
+// by synchronous calls on large host buffers.
+int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>& hp, size_t bytes, hipStream_t s) {
+  static const bool two_d = env_int("ECGPU_PIPE_2D", 1) != 0;
+  const size_t n = hp.size();
+  for (size_t a = 0; a < n;) {
+    size_t b = a + 1;  // [a, b): maximal run with one pitch >= bytes
+    const ptrdiff_t pitch = b < n ? hp[b] - hp[a] : 0;
+    // pageable memory only when the run is contiguous (pitch == bytes): a
+    // pageable 2-D copy with gaps between rows ran 15x slower than per-shard
+    // copies (RS(6,3) 1 MiB, shards malloc'd one by one, 16 B apart)
+    bool ok = two_d && pitch > 0 && size_t(pitch) >= bytes;
+    if (ok && size_t(pitch) != bytes) {
+      hipPointerAttribute_t attr;
+      if (hipPointerGetAttributes(&attr, hp[a]) != hipSuccess) {
+        (void)hipGetLastError();
+        ok = false;
+      } else {
+        ok = attr.type == hipMemoryTypeHost;  // pinned or registered
+      }
+    }
+    if (ok)
+      while (b < n && hp[b] - hp[b - 1] == pitch) ++b;
+    uint8_t* d = d0 + a * dstride;
+    if (b - a >= 2) {
+      // HIP rejects (at enqueue) a 2-D copy whose host span crosses
+      // allocations it knows separately, e.g. shards registered one by one:
+      // those go shard by shard below
+      const hipError_t e =
+          h2d ? hipMemcpy2DAsync(d, dstride, hp[a], size_t(pitch), bytes, b - a, hipMemcpyHostToDevice, s)
+              : hipMemcpy2DAsync(hp[a], size_t(pitch), d, dstride, bytes, b - a, hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) {
+        a = b;
+        continue;
+      }
+      if (e != hipErrorInvalidValue) return fail(ECGPU_ERR_HIP, std::string("hipMemcpy2DAsync: ") + hipGetErrorString(e));
+      (void)hipGetLastError();
+    }
+    for (size_t i = a; i < b; ++i) {
+      if (h2d)
+        ECGPU_HIP(hipMemcpyAsync(d0 + i * dstride, hp[i], bytes, hipMemcpyDefault, s));
+      else
+        ECGPU_HIP(hipMemcpyAsync(hp[i], d0 + i * dstride, bytes, hipMemcpyDefault, s));
+    }
+    a = b;
+  }
+  return ECGPU_OK;
+}
+
+
 // Runs a fused op synchronously over `size` bytes of every buffer.
 int execute(const FusedOp& op, int64_t size) {
   if (op.w != 8 && size % (op.w / 8) != 0)
@@ -700,17 +754,18 @@ int execute(const FusedOp& op, int64_t size) {
   const bool bounce = nstage > 0 && nstage * slot <= bounce_max();
   if (bounce && (rc = ensure_bounce(c, nstage * slot)) != ECGPU_OK) return rc;
   auto bounce_of = [&](size_t i) { return c->bounce + (devp[i] - c->stage); };
-  size_t staged_src = 0;
+  // staged sources occupy slots 0, 1, ... in order: from a stripe buffer
+  // (the client's data shards, client_main.cpp:1619-1647) ONE 2-D copy
+  std::vector<char*> staged_hp;
   for (size_t j = 0; j < op.srcs.size(); ++j)
     if (staged[j]) {
-      ++staged_src;
-      if (bounce)
-        std::memcpy(bounce_of(j), op.srcs[j], size_t(size));
-      else
-        ECGPU_HIP(hipMemcpyAsync(devp[j], op.srcs[j], size_t(size), hipMemcpyHostToDevice, c->stream));
+      staged_hp.push_back(static_cast<char*>(op.srcs[j]));
+      if (bounce) std::memcpy(bounce_of(j), op.srcs[j], size_t(size));
     }
-  if (bounce && staged_src > 0)
-    ECGPU_HIP(hipMemcpyAsync(c->stage, c->bounce, staged_src * slot, hipMemcpyHostToDevice, c->stream));
+  if (bounce && !staged_hp.empty())
+    ECGPU_HIP(hipMemcpyAsync(c->stage, c->bounce, staged_hp.size() * slot, hipMemcpyHostToDevice, c->stream));
+  else if ((rc = copy_shards(true, c->stage, slot, staged_hp, size_t(size), c->stream)) != ECGPU_OK)
+    return rc;
 
   std::vector<const uint8_t*> sp(static_cast<size_t>(nsrc));
   std::vector<uint8_t*> dp(static_cast<size_t>(rows));
@@ -732,13 +787,30 @@ int execute(const FusedOp& op, int64_t size) {
     rc = plan_launch(p, c->stream);
     if (rc != ECGPU_OK) return rc;
   }
+  std::vector<char*> out_hp;  // staged outputs in consecutive slots: one 2-D copy back
+  uint8_t* out_d0 = nullptr;
+  bool out_run = !bounce;
   for (int r = 0; r < rows; ++r) {
     const size_t i = size_t(std::find(bufs.begin(), bufs.end(), op.dsts[r]) - bufs.begin());
     if (via_temp)
       ECGPU_HIP(hipMemcpyAsync(devp[i], dp[r], size_t(size), hipMemcpyDeviceToDevice, c->stream));
-    if (staged[i])
-      ECGPU_HIP(hipMemcpyAsync(bounce ? static_cast<void*>(bounce_of(i)) : op.dsts[r], devp[i], size_t(size),
-                               hipMemcpyDeviceToHost, c->stream));
+    if (!staged[i]) continue;
+    if (bounce) {
+      ECGPU_HIP(hipMemcpyAsync(bounce_of(i), devp[i], size_t(size), hipMemcpyDeviceToHost, c->stream));
+      continue;
+    }
+    if (out_hp.empty()) out_d0 = devp[i];
+    out_run &= devp[i] == out_d0 + out_hp.size() * slot;
+    out_hp.push_back(static_cast<char*>(op.dsts[r]));
+  }
+  if (out_run) {
+    if ((rc = copy_shards(false, out_d0, slot, out_hp, size_t(size), c->stream)) != ECGPU_OK) return rc;
+  } else {
+    for (int r = 0; r < rows; ++r) {
+      const size_t i = size_t(std::find(bufs.begin(), bufs.end(), op.dsts[r]) - bufs.begin());
+      if (staged[i] && !bounce)
+        ECGPU_HIP(hipMemcpyAsync(op.dsts[r], devp[i], size_t(size), hipMemcpyDeviceToHost, c->stream));
+    }
   }
   ECGPU_HIP(hipStreamSynchronize(c->stream));
   ECGPU_HIP(hipGetLastError());
@@ -999,6 +1071,7 @@ ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create_decode(int k, int m, int w, cons
   return pipeline_build(k, m, n_out, n_src, coef.data(), src.data(), out.data(), size, depth, device);
 }
 
+
 ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, char** coding_ptrs) {
   if (!p || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_submit: bad arguments");
   std::lock_guard<std::mutex> lk(p->mu);
@@ -1010,9 +1083,11 @@ ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, cha
   if (rc != ECGPU_OK) return rc;
   const int ns = p->nsrc(), nr = p->rows();
   const size_t bytes = size_t(p->size);
-  if (nr > 0)  // nothing to read when no shard is written
-    for (int j = 0; j < ns; ++j)
-      ECGPU_HIP(hipMemcpyAsync(p->slot_shard(sl, j), host(p->src_ids[j]), bytes, hipMemcpyDefault, p->s_h2d));
+  std::vector<char*> hp;
+  if (nr > 0) {  // nothing to read when no shard is written
+    for (int j = 0; j < ns; ++j) hp.push_back(host(p->src_ids[j]));
+    if ((rc = copy_shards(true, p->slot_shard(sl, 0), p->slot_stride, hp, bytes, p->s_h2d)) != ECGPU_OK) return rc;
+  }
   ECGPU_HIP(hipEventRecord(p->loaded[sl], p->s_h2d));
   ECGPU_HIP(hipStreamWaitEvent(p->s_comp, p->loaded[sl], 0));
   if (ns > 0 && nr > 0) {
@@ -1024,8 +1099,9 @@ ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, cha
   }
   ECGPU_HIP(hipEventRecord(p->computed[sl], p->s_comp));
   ECGPU_HIP(hipStreamWaitEvent(p->s_d2h, p->computed[sl], 0));
-  for (int i = 0; i < nr; ++i)
-    ECGPU_HIP(hipMemcpyAsync(host(p->out_ids[i]), p->slot_shard(sl, ns + i), bytes, hipMemcpyDefault, p->s_d2h));
+  hp.clear();
+  for (int i = 0; i < nr; ++i) hp.push_back(host(p->out_ids[i]));
+  if ((rc = copy_shards(false, p->slot_shard(sl, ns), p->slot_stride, hp, bytes, p->s_d2h)) != ECGPU_OK) return rc;
   ECGPU_HIP(hipEventRecord(p->drained[sl], p->s_d2h));
   p->slot_ticket[sl] = t;
   p->next_ticket = t + 1;

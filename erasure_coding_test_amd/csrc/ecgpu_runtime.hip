@@ -96,22 +96,26 @@ hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t 
 // Residency cap for the streaming kernels.  Fewer resident workgroups per CU
 // means fewer DRAM pages open at once across the chip: with each lane reading
 // K shards and writing R, the uncapped kernel (VGPR-limited to 7 blocks/CU)
-// keeps ~28k distinct 4 KiB shard chunks in flight.  3 blocks/CU measured
-// (DESIGN.md §5): decode{0} +9 %, RS(6,3) 1 MiB encode +6 %, RS(10,4) and
-// RS(12,4) encode neutral; a launch dense in GF multiplies (decode{0,1,2,3}:
-// 40 non-unit coefficients over 14 shards) needs the occupancy to hide its
-// VALU work and loses 7 %, so such launches stay uncapped (cap_for).  The
-// cap is an unused dynamic LDS allocation of LDS_per_CU / blocks (rounded
-// down to 512 B).  ECGPU_BLOCKS_PER_CU overrides the block count (0 = never).
-unsigned residency_lds_bytes(int device) {
+// keeps ~28k distinct 4 KiB shard chunks in flight.  What matters is the
+// number of shard streams per CU, blocks x (K + R): about 40 is best
+// (profiles/r01_residency_streams.json): RS(10,4) encode (14
+// streams) and decode{0} (11) at 3 blocks/CU (+9 % on decode{0} vs
+// uncapped), RS(6,3) (9 streams) at 4 (+6 % vs 3), never fewer than 3.  A
+// launch dense in GF multiplies (decode{0,1,2,3}: 40 non-unit coefficients
+// over 14 shards) needs the occupancy to hide its VALU work and loses 7 %,
+// so such launches stay uncapped (cap_for).  The cap is an unused dynamic
+// LDS allocation of LDS_per_CU / blocks (rounded down to 512 B).
+// ECGPU_BLOCKS_PER_CU fixes the block count (0 = never cap).
+unsigned residency_lds_bytes(int device, int streams) {
   static std::once_flag once;
   static int per_cu = 0;
-  static int blocks = 0;
+  static int fixed = -1;
   std::call_once(once, [&] {
     if (hipDeviceGetAttribute(&per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess)
       per_cu = 0;
-    blocks = env_int("ECGPU_BLOCKS_PER_CU", 3);
+    fixed = env_int("ECGPU_BLOCKS_PER_CU", -1);
   });
+  const int blocks = fixed >= 0 ? fixed : std::max(3, 40 / std::max(1, streams));
   if (blocks <= 0 || per_cu <= 0) return 0;
   const unsigned b = unsigned(per_cu / blocks) & ~511u;
   return b > unsigned(per_cu / (blocks + 1)) ? b : 0u;
@@ -481,7 +485,7 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
       if (nvec > 0) {
         const int64_t per_block = int64_t(dev::kBlock) * vec;
         const dim3 grid(unsigned((nvec + per_block - 1) / per_block), unsigned(ns));
-        const unsigned lds = cap ? residency_lds_bytes(p->device) : 0u;
+        const unsigned lds = cap ? residency_lds_bytes(p->device, K + R) : 0u;
         ECGPU_HIP(launch(vec_fn, grid, block, a, stream, lds));
       }
       if (byte0 < p->size) {

@@ -334,11 +334,7 @@ int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* co
   return ECGPU_OK;
 }
 
-// w = 16 / 32: 16-B column kernel over the aligned part, word kernel for the
-// rest; size must be a whole number of words (checked by the callers).  The
-// column kernel is gf_apply_wide_nib (LDS nibble tables) when a launch's
-// tables fit in kNibMaxLds, else gf_apply_wide (v_perm); ECGPU_WIDE=1 forces
-// v_perm (A/B, tools/bench_surface.py).
+// CU count (the launch device; the pool is homogeneous).
 int multiprocessors(int device) {
   static std::once_flag once;
   static int n = 0;
@@ -366,6 +362,11 @@ int resident_blocks(KernelFn fn, unsigned lds) {
   return n;
 }
 
+// w = 16 / 32: 16-B column kernel over the aligned part, word kernel for the
+// rest; size must be a whole number of words (checked by the callers).  The
+// column kernel is gf_apply_wide_nib (LDS nibble tables) when a launch's
+// tables fit in kNibMaxLds, else gf_apply_wide (v_perm); ECGPU_WIDE=1 forces
+// v_perm (A/B, tools/bench_surface.py).
 int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
   const int K = p->nsrc, W = p->w / 8, nw = wide_words_per_coef(p->w);
   const int64_t nvec = p->aligned ? p->size / 16 : 0;

@@ -1,56 +1,152 @@
-"""Headline benchmark: device-resident RS(10,4) encode + decode, 4 MiB shards.
+"""Headline benchmark: device-resident RS encode (+ decode), one rank per GPU.
 
 BASELINE.json metric: "GiB/s device-resident RS encode+decode, RS(10,4) 4 MiB
 shards, 1/2/4/8 GPU".  One step = one pass of the hot path over one batch of
 synthetic stripes resident in HBM:
 
-  encode  : B stripes x (10 data -> 4 parity)          (jerasure_matrix_encode)
-  decode  : B stripes, data shard 0 erased, rebuilt from the first 10
-            survivors (jerasure_matrix_decode, row_k_ones=0 -- the client's
-            call, client_main.cpp:2118)
+  --config C3 (default; the metric's workload)
+     encode  : B stripes x (10 data -> 4 parity)          (jerasure_matrix_encode)
+     decode  : B stripes, data shard 0 erased, rebuilt from the first 10
+               survivors (jerasure_matrix_decode, row_k_ones=0 -- the client's
+               call, client_main.cpp:2118)
+  --config C5 (BASELINE.json configs[4])
+     encode  : 8 stripes/GPU x RS(12,4), 16 MiB shards
 
 value = user-data bytes processed by all ranks / wall time of the K timed
-steps (max over ranks) = N * K * B * 2 * k * S / t, in GiB/s.  Stripes are
-independent, so each rank codes its own B stripes (weak scaling, no data-path
-collective); the only cross-rank traffic is the timing barrier and one
-max-reduce on the host (gloo).
+steps (max over ranks), in GiB/s.  Stripes are independent, so each rank codes
+its own stripes -- global stripe ids round-robin over ranks (rank r owns ids
+r, r+N, ...), the reference's byte-range / stripe splitting
+(client_main.cpp:1074-1164, ecx_datanode_main.cpp:1113-1117) mapped onto GPUs
+-- with no data-path collective (weak scaling); the only cross-rank traffic is
+the timing barrier, one max-reduce and the per-rank report, on gloo (host).
 
-    python bench.py [--gpus N --steps K --warmup W --stripes B]
-    torchrun --nproc-per-node N bench.py --gpus N ...        (N > 1)
+Launch:
+    python bench.py                                  N = 1, in process
+    python bench.py --gpus N                         spawns N rank processes
+                                                     (one per visible GPU) itself
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+                                                     the driver's form; ranks
+                                                     come from the environment
+--gpus N with fewer than N visible GPUs exits non-zero, as does a WORLD_SIZE
+that disagrees with --gpus.  ECGPU_BENCH_ONE_DEVICE=1 puts every rank on
+cuda:0 -- a multi-process rehearsal on a one-GPU box, labelled
+"rehearsal": true (not a scaling measurement).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-K_DATA, M_PARITY, SHARD = 10, 4, 4 << 20
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HEADLINE_METRIC = "GiB/s device-resident RS encode+decode, RS(10,4) 4 MiB shards, 1/2/4/8 GPU"
+
+# BASELINE.json configs: (k, m, shard bytes, default stripes per GPU, erasures decoded per step)
+CONFIGS = {
+    "C3": dict(k=10, m=4, shard=4 << 20, stripes=96, erasures=[0], cfg_id=3,
+               metric=HEADLINE_METRIC,
+               workload="RS(10,4) encode + decode{{0}}, 4 MiB shards, {B} stripes/GPU"),
+    "C5": dict(k=12, m=4, shard=16 << 20, stripes=8, erasures=None, cfg_id=5,
+               metric="GiB/s device-resident RS(12,4) encode, 16 MiB shards, stripes sharded across GPUs",
+               workload="C5: RS(12,4) encode, 16 MiB shards, {B} stripes/GPU, global stripe ids round-robin "
+                        "over ranks"),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--stripes", type=int, default=96,
-                    help="stripes per GPU per step (96 x 56 MiB = 5.3 GiB resident; throughput plateaus from 96, "
-                         "DESIGN.md §6)")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="C3")
+    ap.add_argument("--stripes", type=int, default=0,
+                    help="stripes per GPU per step (default: C3 96 x 56 MiB = 5.3 GiB resident -- throughput "
+                         "plateaus from 96, DESIGN.md §6; C5 8 x 256 MiB)")
     ap.add_argument("--kernel", choices=["perm", "lds"], default="perm")
     ap.add_argument("--nt", type=int, default=1, help="non-temporal loads/stores")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
-    return ap.parse_args()
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the per-config block (C2 / C3 / C4 / C5 launches, N = 1 only)")
+    ap.add_argument("--spawn-selftest", action="store_true",
+                    help="launch / rendezvous / report path only, no GPU work (CPU test of --gpus N)")
+    return ap.parse_args(argv)
 
 
-def dist_setup(n_gpus):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+# ------------------------------------------------------------------ launch ----
+def launch_mode(gpus: int, env, device_count: int, selftest: bool = False):
+    """('run' | 'spawn' | 'error', message).  Pure: tested on CPU."""
+    rehearsal = env.get("ECGPU_BENCH_ONE_DEVICE") == "1"
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    world_env = env.get("WORLD_SIZE")
+    if world_env is not None and world_env != "":
+        if int(world_env) != gpus:
+            return "error", f"WORLD_SIZE={world_env} but --gpus {gpus}: launch one rank per GPU"
+        mode = "run"
+    else:
+        mode = "run" if gpus == 1 else "spawn"
+    need = 1 if rehearsal else gpus
+    if not selftest and gpus > 1 and device_count < need:
+        return "error", (f"--gpus {gpus} needs {gpus} visible GPUs, found {device_count} (ECGPU_BENCH_ONE_DEVICE=1 "
+                         f"runs every rank on cuda:0 as a labelled rehearsal)")
+    return mode, ""
+
+
+def rank_envs(n: int, port: int, base) -> list:
+    """Environment of each spawned rank (torch.distributed.run's variables)."""
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out.append(e)
+    return out
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start n rank processes of this script (no GPU touched here) and return
+    the worst exit code; if one rank fails the others are stopped rather than
+    left waiting at a barrier."""
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e)
+             for e in rank_envs(n, free_port(), os.environ)]
+    rc = 0
+    while procs:
+        for p in list(procs):
+            r = p.poll()
+            if r is None:
+                continue
+            procs.remove(p)
+            if r != 0:
+                rc = rc or (r if r > 0 else 1)
+                for q in procs:  # the exact PIDs started above
+                    q.terminate()
+                for q in procs:
+                    try:
+                        q.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                procs = []
+                break
+        time.sleep(0.05)
+    return rc
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1") or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -69,32 +165,33 @@ def barrier(world):
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
+    import torch
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
+def gather(obj, world: int) -> list:
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def stripes_for_rank(total: int, rank: int, world: int) -> list:
-    """Round-robin stripe ids over ranks; used by the
-    multi-rank tests to check every stripe is coded exactly once."""
+    """Global stripe ids owned by a rank: round-robin."""
     return list(range(rank, total, world))
 
 
-def load_traffic(workload: str):
-    """HBM bytes per encode launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_encode.json, written by profiles/summarize.py), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_encode.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
-    return None
+def global_stripe_ids(per_rank: int, rank: int, world: int) -> list:
+    """The per_rank global ids of `rank` when every rank codes per_rank stripes."""
+    return stripes_for_rank(per_rank * world, rank, world)
 
 
+# ------------------------------------------------------------- host info ----
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -114,14 +211,33 @@ def host_has_avx2() -> bool:
         return False
 
 
-def cpu_baseline(seconds: float, threads: int = 1, o3: bool = False):
-    """Reference CPU path on the host: oracle/_ref (the reference's own
-    src/erasure_coding compiled -O2) if shipped, else our C restatement.
-    Bounded sample of the same workload: one RS(10,4) 4 MiB stripe, encode +
-    decode{0}, repeated until `seconds` of wall time.  With threads > 1 each
-    call is split by byte range over threads exactly like the reference
+HOST_THREAD_CAP = 16  # the GPU box's CPU share per GPU (16 per one-GPU lease)
+
+
+def host_cpus() -> list:
+    """CPUs this process may run on (affinity), at most HOST_THREAD_CAP of them:
+    the box's per-GPU CPU share, whatever the machine's total core count."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    return cpus[:HOST_THREAD_CAP] or [0]
+
+
+# ------------------------------------------------------------ CPU baseline ----
+def cpu_baseline(seconds: float, host_stripe, k, m, erasures, threads: int = 1, o3: bool = False):
+    """Reference CPU path on the host cores: oracle/_ref (the reference's own
+    src/erasure_coding compiled -O2, or -O3 -march=x86-64-v3) if shipped, else
+    our C restatement (oracle/ec_oracle.c).  Bounded sample of the same
+    workload: ONE stripe of the GPU slab (copied to the host), encode (+ the
+    step's decode), repeated until `seconds` of wall time.  With threads > 1
+    each call is split by byte range over threads exactly like the reference
     client's encode_mul_thread (client_main.cpp:1074-1164; thread 0 takes the
-    remainder) -- ctypes releases the GIL, so the threads run in parallel."""
+    remainder); each thread is pinned to its own CPU (sched_setaffinity) and
+    ctypes releases the GIL, so the threads run in parallel.
+
+    Also the checker: the CPU's parity (and rebuilt shard) on that stripe must
+    equal what the GPU left in HBM.  Returns (baseline dict, parity_ok)."""
     import ctypes
     import threading
 
@@ -135,13 +251,14 @@ def cpu_baseline(seconds: float, threads: int = 1, o3: bool = False):
             o = Reference()
         except (FileNotFoundError, OSError):
             o = Restatement()
-    k, m, S = K_DATA, M_PARITY, SHARD
+    S = host_stripe.shape[1]
     M = o.vandermonde_coding_matrix(k, m)
-    rng = np.random.default_rng(0)
     data = alloc_shards(k, S)
-    for d in data:
-        d[:S] = rng.integers(0, 256, S, dtype=np.uint8)
+    for j in range(k):
+        data[j][:S] = host_stripe[j]
     coding = alloc_shards(m, S)
+    cpus = host_cpus()
+    threads = max(1, min(threads, len(cpus)))
     ranges, off = [], 0
     for t in range(threads):
         n = S // threads + (S % threads if t == 0 else 0)
@@ -157,38 +274,86 @@ def cpu_baseline(seconds: float, threads: int = 1, o3: bool = False):
     def one(p):
         d, c, n = p
         o.matrix_encode(k, m, M, d, c, n)
-        o.matrix_decode(k, m, M, 0, [0], d, c, n)
+        if erasures:
+            o.matrix_decode(k, m, M, 0, erasures, d, c, n)
 
+    def run(t):
+        os.sched_setaffinity(0, {cpus[t]})  # this thread only (Linux)
+        one(parts[t])
+
+    # one thread per byte range per call, joined per call, like the reference
+    # client (pthread_create / pthread_join around each encode)
     iters, t0 = 0, time.perf_counter()
     while True:
-        if threads == 1:
-            one(parts[0])
-        else:
-            ts = [threading.Thread(target=one, args=(p,)) for p in parts]
-            for t in ts:
-                t.start()
-            for t in ts:
-                t.join()
+        ts = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
         iters += 1
         el = time.perf_counter() - t0
         if el >= seconds or iters >= 2000:
             break
-    gib = iters * 2 * k * S / 2**30
+    ok = all(np.array_equal(coding[i][:S], host_stripe[k + i]) for i in range(m))
+    if erasures:
+        ok = ok and all(np.array_equal(data[j][:S], host_stripe[j]) for j in erasures if j < k)
+    gib = iters * (2 if erasures else 1) * k * S / 2**30
     flags = "-O3 -march=x86-64-v3" if o3 else "-O2"
     src = f"reference src/erasure_coding compiled g++ {flags}" if o.kind == "reference" else "oracle/ec_oracle.c -O2"
-    return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": threads, "kind": o.kind,
-            "sample": f"{iters} x (RS(10,4) 4 MiB stripe encode + decode of erasure {{0}}), {threads} thread(s) "
-                      f"splitting byte ranges like client_main.cpp:1074-1164, {el:.1f} s, {src}, "
-                      f"host CPU {cpu_model()}"}
+    step = f"RS({k},{m}) {S >> 20} MiB stripe encode" + (f" + decode of erasures {set(erasures)}" if erasures else "")
+    cap = f", capped at {HOST_THREAD_CAP} = the box's per-GPU CPU share" if threads > 1 else ""
+    return ({"value": round(gib / el, 4), "unit": "GiB/s", "cores": threads, "kind": o.kind,
+             "sample": f"{iters} x ({step}) on stripe 0 of the GPU slab, {threads} thread(s) pinned one per CPU{cap}, "
+                       f"splitting byte ranges like client_main.cpp:1074-1164, {el:.1f} s, {src}, "
+                       f"host CPU {cpu_model()}"}, ok)
 
 
-def copy_ceiling(slab, reps: int = 10):
+# ----------------------------------------------------------- GPU helpers ----
+def median(xs):
+    s = sorted(xs)
+    n = len(s)
+    return s[n // 2] if n % 2 else 0.5 * (s[n // 2 - 1] + s[n // 2])
+
+
+def time_launches(launch, stream, reps: int, warmup: int = 3) -> float:
+    """Median device time (ms) of `launch` over `reps` runs, HIP events on
+    the launch stream."""
+    import torch
+    for _ in range(warmup):
+        launch()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in evs:
+        e0.record(stream)
+        launch()
+        e1.record(stream)
+    torch.cuda.synchronize(stream.device)
+    return median([e0.elapsed_time(e1) for e0, e1 in evs])
+
+
+def fill_random(slab, ids, cfg_id):
+    """Uniform random bytes per GLOBAL stripe id (zeros would flatter DVFS);
+    the same global stripe gets the same bytes whichever rank owns it."""
+    import torch
+    for b, gid in enumerate(ids):
+        g = torch.Generator(device=slab.device).manual_seed((cfg_id << 40) ^ (gid << 8) ^ 0xEC)
+        slab[b].random_(0, 256, generator=g)
+
+
+def roofline_entry(bytes_per_launch, ms):
+    gbs = bytes_per_launch / (ms / 1e3) / 1e9
+    return {"algorithmic_bytes_per_launch": int(bytes_per_launch), "median_launch_ms": round(ms, 4),
+            "achieved_GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
+def copy_ceiling(slab, shard, reps: int = 10):
     """Measured stream-copy ceiling on this GPU: the
-    diagnostic 16-B non-temporal copy kernel (libecgpu_diag.so, diag_copy)
-    moving shards 0..6 -> 7..13 of every stripe of the bench slab, i.e. the
-    same bytes, shard stride and skew as the coding launches.  Returns GB/s of
-    (read + written) bytes, or None when the diagnostic library is absent."""
+    diagnostic 16-B copy kernel (libecgpu_diag.so, diag_copy) moving the first
+    half of every stripe's shards onto the second half, i.e. the same bytes,
+    shard stride and skew as the coding launches.  GB/s of (read + written)
+    bytes, best of the 4 cache policies, or None without the library."""
     import ctypes
+
+    import torch
 
     from erasure_coding_test_amd import _native as N
     path = os.path.join(N.LIB_DIR, "libecgpu_diag.so")
@@ -199,7 +364,7 @@ def copy_ceiling(slab, reps: int = 10):
     L.ecgpu_diag_launch.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p] * 4 + [
         ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_void_p,
         ctypes.c_void_p]
-    B, n_sh, S = slab.shape[0], slab.shape[1], SHARD
+    B, n_sh = slab.shape[0], slab.shape[1]
     half = n_sh // 2
     dev = slab.device
     src = torch.tensor([slab[b, i].data_ptr() for b in range(B) for i in range(half)], dtype=torch.int64, device=dev)
@@ -208,64 +373,170 @@ def copy_ceiling(slab, reps: int = 10):
     stream = torch.cuda.current_stream(dev)
     best = None
     for policy in range(4):  # bit 0: non-temporal loads, bit 1: non-temporal stores
-        ts = []
-        for i in range(reps + 2):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            rc = L.ecgpu_diag_launch(1, 1, 1, 1, policy, None, None, src.data_ptr(), dst.data_ptr(), B * half, S, 0,
-                                     0, 1, stream.cuda_stream, None)
-            e1.record(stream)
-            torch.cuda.synchronize(dev)
-            if rc != 0:
-                return None
-            if i >= 2:
-                ts.append(e0.elapsed_time(e1))
-        ts.sort()
-        ms = ts[len(ts) // 2]
+        rc = [0]
+
+        def go():
+            rc[0] = rc[0] or L.ecgpu_diag_launch(1, 1, 1, 1, policy, None, None, src.data_ptr(), dst.data_ptr(),
+                                                 B * half, shard, 0, 0, 1, stream.cuda_stream, None)
+        ms = time_launches(go, stream, reps, warmup=2)
+        if rc[0] != 0:
+            return None
         if best is None or ms < best[0]:
             best = (ms, policy)
     ms, policy = best
-    return {"GBps": round(2 * S * B * half / (ms / 1e3) / 1e9, 1), "avg_launch_ms": round(ms, 4),
+    return {"GBps": round(2 * shard * B * half / (ms / 1e3) / 1e9, 1), "median_launch_ms": round(ms, 4),
             "kernel": f"diag_copy 16 B/lane, shards 0..{half - 1} -> {half}..{n_sh - 1} of every stripe; best of the "
                       f"4 cache policies (here loads {'nt' if policy & 1 else 'plain'}, stores "
                       f"{'nt' if policy & 2 else 'plain'}), median of {reps}"}
 
 
-def host_threads() -> int:
-    """The CPU share this process may use (affinity), capped at 16 (the GPU box's per-GPU share)."""
+def load_traffic(name: str, workload_key: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_<name>.json, written by profiles/summarize.py from separate
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command), or None
+    when the summary is for another workload."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
     try:
-        n = len(os.sched_getaffinity(0))
-    except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload_key") == workload_key:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
 
 
-def main():
-    args = parse()
-    rank, local, world = dist_setup(args.gpus)
+def config_block(E, N, dev, stream, kind, nt, main=None):
+    """Every BASELINE.json GPU config as its own launch (median of 20 HIP-event
+    timed launches after warm-up, ≥ 1 GiB streamed per launch): C2 encode,
+    C3 encode / decode{0} (from the timed steps), C4 decode{0,1,2,3} with its
+    host-side plan cost reported separately, C5 encode."""
+    import ctypes
+
+    import torch
+    out = {}
+
+    def encode_cfg(name, k, m, S, B, cfg_id):
+        M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+        slab, shards = E.alloc_stripes(B, k, m, S, dev)
+        fill_random(slab, list(range(B)), cfg_id)
+        p = E.encode_plan(k, m, M, dev.index).bind([st[:k] for st in shards], [st[k:] for st in shards], S)
+        p.set_kernel(kind, nt)
+        ms = time_launches(lambda: p.launch(stream.cuda_stream), stream, 20, warmup=5)
+        e = {"workload": f"RS({k},{m}) encode, {S >> 20} MiB shards, {B} stripes"}
+        e.update(roofline_entry((k + m) * S * B, ms))
+        out[name] = e
+        p.close()
+        del slab, shards
+
+    encode_cfg("C2_encode", 6, 3, 1 << 20, 128, 2)
+    if main is not None:
+        out.update(main)
+    # C4: worst-case decode, erasures {0,1,2,3} of RS(10,4) 4 MiB (10 survivors = ids 4..13)
+    k, m, S, B = 10, 4, 4 << 20, 24
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    slab, shards = E.alloc_stripes(B, k, m, S, dev)
+    fill_random(slab, list(range(B)), 4)
+    er = [0, 1, 2, 3]
+    # host side, reported separately: the decode planning (erasures -> dm_ids ->
+    # k x k GF inversion -> fused map, jerasure.cpp:84-112, :153-254) and the
+    # whole plan creation (planning + coefficient tables + upload)
+    n = k + m
+    outs, srcs, coef = (ctypes.c_int * n)(), (ctypes.c_int * n)(), (ctypes.c_int * (n * n))()
+    no, ns = ctypes.c_int(), ctypes.c_int()
+    Mi, eri = N.int_array(M), N.int_array(er + [-1])
+    host_us = []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        N.lib.ecgpu_decode_plan(k, m, 8, Mi, 0, eri, outs, ctypes.byref(no), srcs, ctypes.byref(ns), coef)
+        host_us.append((time.perf_counter() - t0) * 1e6)
+    create_us = []
+    for _ in range(20):
+        t0 = time.perf_counter()
+        dp = E.DecodePlan(k, m, M, er, 0, dev.index)
+        create_us.append((time.perf_counter() - t0) * 1e6)
+        dp.close()
+    dp = E.DecodePlan(k, m, M, er, 0, dev.index).bind_stripes(shards, S)
+    dp.set_kernel(kind, nt)
+    ms = time_launches(lambda: dp.launch(stream.cuda_stream), stream, 20, warmup=5)
+    e = {"workload": f"RS(10,4) decode of erasures {{0,1,2,3}}, 4 MiB shards, {B} stripes (10 survivors read, "
+                     f"4 shards written)"}
+    e.update(roofline_entry((k + len(er)) * S * B, ms))
+    e["host_decode_plan_us"] = round(median(host_us), 2)
+    e["host_plan_create_us"] = round(median(create_us), 2)
+    e["host_note"] = ("host_decode_plan_us: ecgpu_decode_plan (survivor choice, k x k inversion, fused map) through "
+                      "ctypes; host_plan_create_us: the whole DecodePlan incl. coefficient tables and their upload; "
+                      "medians, not in the launch time")
+    out["C4_decode_0123"] = e
+    dp.close()
+    del slab, shards
+    encode_cfg("C5_encode", 12, 4, 16 << 20, 8, 5)
+    torch.cuda.synchronize(dev)
+    return out
+
+
+# -------------------------------------------------------------------- main ----
+def selftest_main(args):
+    """--spawn-selftest: the multi-rank control path without a GPU."""
+    rank, local, world = dist_setup()
+    barrier(world)
+    t = max_over_ranks(float(rank + 1), world)
+    per_rank = gather({"rank": rank, "local_rank": local, "world": world, "pid": os.getpid()}, world)
+    if rank == 0:
+        print(json.dumps({"selftest": True, "n_gpus": world, "max_over_ranks": t, "per_rank": per_rank,
+                          "stripes": {r: global_stripe_ids(2, r, world) for r in range(world)}}), flush=True)
+    barrier(world)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    rehearsal = os.environ.get("ECGPU_BENCH_ONE_DEVICE") == "1"
+    import torch
+    count = 0 if args.spawn_selftest else torch.cuda.device_count()  # does not initialise the GPU
+    mode, msg = launch_mode(args.gpus, os.environ, count, args.spawn_selftest)
+    if mode == "error":
+        print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+        return 2
+    if mode == "spawn":
+        return spawn_ranks(args.gpus, argv)
+    if args.spawn_selftest:
+        return selftest_main(args)
+
+    rank, local, world = dist_setup()
     import erasure_coding_test_amd as E
     from erasure_coding_test_amd import _native as N
 
-    # ECGPU_BENCH_ONE_DEVICE=1: every rank on cuda:0 -- a multi-rank rehearsal
-    # on a one-GPU box (the numbers are then not a scaling measurement).
-    if os.environ.get("ECGPU_BENCH_ONE_DEVICE") == "1":
+    if rehearsal:
         local = 0
+    elif local >= count:
+        print(f"bench.py: rank {rank} has LOCAL_RANK {local} but only {count} GPUs are visible", file=sys.stderr)
+        return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    k, m, S, B = K_DATA, M_PARITY, SHARD, args.stripes
+    C = CONFIGS[args.config]
+    k, m, S = C["k"], C["m"], C["shard"]
+    B = args.stripes or C["stripes"]
+    erasures = C["erasures"]
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
 
     # B stripes x (k+m) shards in one HBM slab at the library's recommended
-    # shard stride (S + 4 KiB skew); random data (zeros would flatter DVFS).
+    # shard stride (S + 10 KiB skew); global stripe ids round-robin over ranks
+    ids = global_stripe_ids(B, rank, world)
     slab, shards = E.alloc_stripes(B, k, m, S, dev)
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    slab.random_(0, 256, generator=g)
+    fill_random(slab, ids, C["cfg_id"])
 
     kind = N.KERNEL_LDS if args.kernel == "lds" else N.KERNEL_PERM
     enc = E.encode_plan(k, m, M, local).bind([st[:k] for st in shards], [st[k:] for st in shards], S)
     enc.set_kernel(kind, bool(args.nt))
-    dec = E.DecodePlan(k, m, M, [0], 0, local).bind_stripes(shards, S)
-    dec.set_kernel(kind, bool(args.nt))
+    dec = None
+    if erasures:
+        dec = E.DecodePlan(k, m, M, erasures, 0, local).bind_stripes(shards, S)
+        dec.set_kernel(kind, bool(args.nt))
     stream = torch.cuda.current_stream(dev)
 
     def step(ev=None):
@@ -274,9 +545,10 @@ def main():
         enc.launch(stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
-        dec.launch(stream.cuda_stream)
-        if ev is not None:
-            ev[2].record(stream)
+        if dec is not None:
+            dec.launch(stream.cuda_stream)
+            if ev is not None:
+                ev[2].record(stream)
 
     for _ in range(args.warmup):
         step()
@@ -296,42 +568,63 @@ def main():
     barrier(world)
     t = max_over_ranks(elapsed, world)
 
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    enc_bytes = (k + m) * S * B           # algorithmic HBM bytes per encode launch
-    dec_bytes = (k + 1) * S * B           # 10 survivors read + 1 shard written
-    user_bytes = world * args.steps * B * 2 * k * S
-    value = user_bytes / t / 2**30
+    enc_ms = median([e[0].elapsed_time(e[1]) for e in evs])
+    dec_ms = median([e[1].elapsed_time(e[2]) for e in evs]) if dec is not None else None
+    enc_bytes = (k + m) * S * B  # algorithmic HBM bytes per encode launch
+    dec_bytes = (k + len(erasures)) * S * B if erasures else 0  # k survivors read + erased shards written
+    user_per_stripe = (2 if erasures else 1) * k * S
+    value = world * args.steps * B * user_per_stripe / t / 2**30
 
-    # sanity: the decode must have rebuilt shard 0 bit-exactly (it is rewritten
-    # every step from the survivors; compare with an independent encode check)
-    ok = True
+    # independent check of the timed result on every rank: stripe 0 re-encoded
+    # with the OTHER multiply engine (LDS nibble tables, gf_apply_lds), outside
+    # the timed region and its statistics
+    chk = torch.empty((m, S), dtype=torch.uint8, device=dev)
+    ref = E.encode_plan(k, m, M, local).bind([shards[0][:k]], [[chk[i] for i in range(m)]], S)
+    ref.set_kernel(N.KERNEL_LDS if kind == N.KERNEL_PERM else N.KERNEL_PERM, True)
+    ref.launch(stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    ok = all(bool(torch.equal(chk[i], shards[0][k + i])) for i in range(m))
+    host_stripe = slab[0, :, :S].cpu().numpy() if (rank == 0 and world == 1 and args.cpu_seconds > 0) else None
+
+    per_rank = gather({"rank": rank, "device": local, "elapsed_s": round(elapsed, 6),
+                       "encode_median_ms": round(enc_ms, 4),
+                       "decode_median_ms": round(dec_ms, 4) if dec_ms is not None else None,
+                       "stripe_ids": [ids[0], ids[-1], len(ids)], "parity_ok": ok}, world)
+    ok = all(p["parity_ok"] for p in per_rank)
+
+    copy = None
+    configs = None
     if rank == 0:
-        # re-encode stripe 0 with the OTHER multiply engine (LDS nibble tables,
-        # gf_apply_lds) so the check is independent of the timed kernel and its
-        # launch does not mix into the timed kernel's rocprof statistics
-        chk = torch.empty((m, S), dtype=torch.uint8, device=dev)
-        ref = E.encode_plan(k, m, M, local).bind([shards[0][:k]], [[chk[i] for i in range(m)]], S)
-        ref.set_kernel(N.KERNEL_LDS, True)
-        ref.launch(stream.cuda_stream)
-        torch.cuda.synchronize(dev)
-        ok = all(bool(torch.equal(chk[i], shards[0][k + i])) for i in range(m))
-        # after the parity check: the copy overwrites the slab
-        copy = copy_ceiling(slab)
+        copy = copy_ceiling(slab, S)  # after the parity checks: the copy overwrites the slab's second half
+        if world == 1 and not args.no_configs:
+            main_entries = {}
+            if args.config == "C3":
+                e = {"workload": f"RS(10,4) encode, 4 MiB shards, {B} stripes (the timed steps)"}
+                e.update(roofline_entry(enc_bytes, enc_ms))
+                main_entries["C3_encode"] = e
+                e = {"workload": f"RS(10,4) decode of erasure {{0}}, 4 MiB shards, {B} stripes (the timed steps)"}
+                e.update(roofline_entry(dec_bytes, dec_ms))
+                main_entries["C3_decode_0"] = e
+            del enc, dec, ref
+            configs = config_block(E, N, dev, stream, kind, bool(args.nt), main_entries)
 
-    workload = f"RS(10,4) encode + decode{{0}}, 4 MiB shards, {B} stripes/GPU"
+    workload = C["workload"].format(B=B)
     if rank == 0:
         cpu = cpu_all = cpu_o3 = None
-        if world == 1 and args.cpu_seconds > 0:
-            cpu = cpu_baseline(args.cpu_seconds)
-            cpu_all = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_threads())
+        cpu_ok = None
+        if host_stripe is not None:
+            cpu, cpu_ok = cpu_baseline(args.cpu_seconds, host_stripe, k, m, erasures)
+            cpu_all, ok_all = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_stripe, k, m, erasures,
+                                           threads=HOST_THREAD_CAP)
+            cpu_ok = cpu_ok and ok_all
             from oracle.oracle import REFERENCE_O3_SO
             if host_has_avx2() and os.path.exists(REFERENCE_O3_SO):
-                cpu_o3 = cpu_baseline(max(2.0, args.cpu_seconds / 2), 1, o3=True)
+                cpu_o3, ok_o3 = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_stripe, k, m, erasures, o3=True)
+                cpu_ok = cpu_ok and ok_o3
         achieved = enc_bytes / (enc_ms / 1e3) / 1e9
-        traffic = load_traffic(workload)
+        wkey = f"{args.config}:{B}"
         out = {
-            "metric": "GiB/s device-resident RS encode+decode, RS(10,4) 4 MiB shards, 1/2/4/8 GPU",
+            "metric": C["metric"],
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -342,32 +635,39 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (uniform random bytes, device-generated)",
+            "data": "synthetic (uniform random bytes, device-generated per global stripe id)",
             "config": {"workload": workload, "k": k, "m": m, "shard_bytes": S, "stripes_per_gpu": B,
                        "shard_stride_bytes": int(slab.stride(1)),
-                       "erasures": [0], "kernel": args.kernel, "nontemporal": bool(args.nt),
-                       "parallelism": f"stripes sharded over {world} GPU(s), no collective"},
+                       "erasures": erasures, "kernel": args.kernel, "nontemporal": bool(args.nt),
+                       "parallelism": f"stripes round-robin over {world} GPU(s), no collective"},
+            "rehearsal": rehearsal,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic("encode", wkey),
                          "kernel": "gf_apply (encode launch)", "algorithmic_bytes_per_launch": enc_bytes,
-                         "avg_launch_ms": round(enc_ms, 4),
+                         "median_launch_ms": round(enc_ms, 4), "kernel_time_stat": "median of HIP events",
                          # the north star's read-only accounting: data-shard bytes only, which
-                         # caps at k/(k+m) = 0.714 of peak for any encode
+                         # caps at k/(k+m) of peak for any encode
                          "read_only_frac": round(k * S * B / (enc_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
             "copy_ceiling": copy,
             "encode_frac_of_copy": round(achieved / copy["GBps"], 4) if copy else None,
-            "decode_kernel": {"avg_launch_ms": round(dec_ms, 4), "algorithmic_bytes_per_launch": dec_bytes,
-                              "achieved_GBps": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1)},
+            "decode_kernel": ({"erasures": erasures, "median_launch_ms": round(dec_ms, 4),
+                               "algorithmic_bytes_per_launch": dec_bytes,
+                               "achieved_GBps": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),
+                               "traffic": load_traffic("decode", wkey)} if dec_ms is not None else None),
+            "per_rank": per_rank,
+            "configs": configs,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "cpu_baseline_o3": cpu_o3,
             "selfcheck_parity_ok": ok,
+            "selfcheck_vs_reference_cpu": cpu_ok,
         }
         print(json.dumps(out), flush=True)
+    barrier(world)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
-    return 0 if ok else 1
+    return 0 if ok and cpu_ok is not False else 1
 
 
 if __name__ == "__main__":

@@ -128,8 +128,8 @@ unsigned residency_lds_bytes(int device, int streams) {
 //   * residency cap unless the launch is dense in GF multiplies (more than
 //     2.5 non-unit coefficients per shard touched): decode{0} +9 %, RS(6,3)
 //     +6 %; the 40-multiply decode{0,1,2,3} needs the occupancy (-7 % capped).
-// The store policy is the plan's `nt` field (0 plain, 1 nt -- the default --
-// 2 sc1, 3 sc0 sc1; ECGPU_NT, ecgpu_plan_set_kernel); ECGPU_CAP (0 = never,
+// The store policy is the plan's `nt` field (0 plain, 1 nt -- the default;
+// ECGPU_NT, ecgpu_plan_set_kernel); ECGPU_CAP (0 = never,
 // 1 = always) overrides the cap rule.
 bool cap_for(int K, int R, int mul_terms) {
   static const int v = env_int("ECGPU_CAP", -1);

@@ -98,20 +98,14 @@ __device__ __forceinline__ u32x4 load16t(const uint8_t* p, int64_t col) {
   else return *a;
 }
 
-// Store cache policy POL: 0 plain, 1 non-temporal (`nt`), 2 `sc1`, 3
-// `sc0 sc1` (written through, not kept in the XCD's L2: MI355X_MICROARCH.md
-// "stores of each flavour").  No builtin expresses sc0/sc1, so 2 and 3 are
-// inline-asm vector stores followed by s_nop 1: a VALU write to the data
-// VGPRs of an in-flight store wider than 8 bytes needs wait states, which the
-// compiler inserts after its own stores but not after inline asm.
+// Store cache policy POL: 0 plain, 1 non-temporal (`nt`).  (Stores that
+// bypass the XCD's L2 -- `sc1`, `sc0 sc1`, inline asm -- were probed in round
+// 1 and were equal or slower in the bench's back-to-back launches, DESIGN.md
+// §5; they live only in the diagnostic library.)
 template <int POL>
 __device__ __forceinline__ void store16t(uint8_t* p, int64_t col, const u32x4& v) {
   gu32x4* a = (gu32x4*)p + col;
-  if constexpr (POL == 3) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(p + col * 16), "v"(v) : "memory");
-  } else if constexpr (POL == 2) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p + col * 16), "v"(v) : "memory");
-  } else if constexpr (POL == 1) {
+  if constexpr (POL == 1) {
     __builtin_nontemporal_store(v, a);
   } else {
     *a = v;
@@ -441,7 +435,7 @@ __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
 }
 
 // Cache policy: NT bit 0 = non-temporal loads, NT >> 1 = store policy
-// (store16t: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1).  The production
+// (store16t: 0 plain, 1 nt).  The production
 // instantiations (gf_spec.hip) all load `nt` and select the store policy per
 // launch.
 template <int K, int R, int UNITS, int VEC = 1, int SLICES = 3, int NT = 3>

@@ -16,7 +16,7 @@ constexpr int kUnitVariants[5] = {dev::kUnitNone, dev::kUnitCol0, dev::kUnitRow0
                                   dev::kUnitAll};
 
 // NT: loads always non-temporal (bit 0), NT >> 1 = store policy
-// (gf_kernels.hpp store16t: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1)
+// (gf_kernels.hpp store16t: 0 plain, 1 nt)
 template <int K, int U, int STORE>
 constexpr SpecKernelFn apply_fn() { return &dev::gf_apply<K, kR, kUnitVariants[U], 1, 3, 1 | (STORE << 1)>; }
 
@@ -28,8 +28,7 @@ struct Pol {
 
 template <int K>
 struct Row {
-  static constexpr const SpecKernelFn* apply[kStorePolicies] = {Pol<K, 0>::apply, Pol<K, 1>::apply,
-                                                                Pol<K, 2>::apply, Pol<K, 3>::apply};
+  static constexpr const SpecKernelFn* apply[kStorePolicies] = {Pol<K, 0>::apply, Pol<K, 1>::apply};
   static constexpr SpecKernelFn lds = &dev::gf_apply_lds<K, kR>;
 };
 

@@ -9,10 +9,10 @@
 namespace ecgpu {
 
 using SpecKernelFn = void (*)(dev::ApplyArgs);
-constexpr int kStorePolicies = 4;
+constexpr int kStorePolicies = 2;
 
-// store_pol: store cache policy of the production kernel, 0 plain, 1 nt,
-// 2 sc1, 3 sc0 sc1 (gf_kernels.hpp store16t; loads are always
+// store_pol: store cache policy of the production kernel, 0 plain, 1 nt
+// (gf_kernels.hpp store16t; loads are always
 // non-temporal).  lds: the LDS nibble-table kernel instead.
 // unit_variant indexes kUnitVariants (ecgpu_runtime.hip).  nullptr if K is
 // outside 1..kMaxSpecK.

@@ -160,8 +160,7 @@ ECGPU_API int ecgpu_plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* 
                               int64_t size);
 /* kind: ECGPU_KERNEL_PERM (production) or ECGPU_KERNEL_LDS; nontemporal: store
  * cache policy of the production kernel: 0 plain, 1 non-temporal (the
- * default), 2 sc1, 3 sc0 sc1 (written through, not kept in L2); its loads are
- * always non-temporal. */
+ * default; larger values clamp to 1); its loads are always non-temporal. */
 ECGPU_API int ecgpu_plan_set_kernel(ecgpu_plan* p, int kind, int nontemporal);
 ECGPU_API int ecgpu_plan_launch(ecgpu_plan* p, void* stream);
 ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p);

@@ -17,6 +17,8 @@ REFERENCE_ROOT = "/root/reference"
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box with -m gpu)")
+    import refcheck
+    refcheck.configure(config)
 
 
 @pytest.fixture(scope="session")
@@ -43,7 +45,8 @@ def reference():
     try:
         return Reference()
     except (FileNotFoundError, OSError):
-        pytest.skip("oracle/_ref not built (needs /root/reference at build time)")
+        import refcheck
+        refcheck.reference_missing("oracle/_ref/libjerasure_ref.so")
 
 
 @pytest.fixture(scope="session")

@@ -32,7 +32,7 @@ def _worker(rank, world, port, total, q):
     from ecdata import fnv1a64, shard_seed, splitmix_bytes
     from oracle.oracle import Restatement, alloc_shards
 
-    r, local, w = bench.dist_setup(world)
+    r, local, w = bench.dist_setup()
     assert (r, w) == (rank, world)
     o = Restatement()
     k, m, size = 6, 3, 1000

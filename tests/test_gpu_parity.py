@@ -656,7 +656,8 @@ def _ref_nsa():
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
                         "libjerasure_ref_nsa.so")
     if not os.path.exists(path):
-        pytest.skip("oracle/_ref/libjerasure_ref_nsa.so not built")
+        import refcheck
+        refcheck.reference_missing("oracle/_ref/libjerasure_ref_nsa.so")
     L = ctypes.CDLL(path)
     I, IP, PP = ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p)
     L._Z22jerasure_matrix_encodeiiiPiPPcS1_i.argtypes = [I, I, I, IP, PP, PP, I]

@@ -1,0 +1,176 @@
+"""The product library under more than one rank, on the GPU.
+
+SURVEY.md §8e: stripes are independent, so ranks shard them round-robin
+(rank r codes global stripe ids r, r+N, ...) with no data-path collective.
+Here two rank processes share cuda:0 (the one-GPU box) and each codes its own
+stripes through the library -- batched plan encode, the fused decode of
+erasures {0,1,2,3} (C4's pattern), and the synchronous drop-in decode -- and
+the union of their results is checked against the CPU oracle on the same
+seeded stripes: every stripe coded exactly once, bytes identical.
+
+Also bench.py's own multi-rank entry point: `--gpus 2` with the one-device
+rehearsal flag spawns two ranks and reports both; without it a one-GPU box
+refuses with a non-zero exit; `--config C5` runs and names C5.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+K, M_PAR, SIZE, TOTAL, CFG = 10, 4, (256 << 10) + 48, 6, 21
+ERASED = [0, 1, 2, 3]
+DROPIN_ERASED = [1, 5, 11]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        import torch
+
+        import bench
+        import erasure_coding_test_amd as E
+        from ecdata import fnv1a64, shard_seed, splitmix_bytes
+
+        r, _, w = bench.dist_setup()
+        assert (r, w) == (rank, world)
+        torch.cuda.set_device(0)  # both ranks on the one GPU of the box
+        dev = torch.device("cuda", 0)
+        ids = bench.stripes_for_rank(TOTAL, rank, world)
+        Mx = E.reed_sol.reed_sol_vandermonde_coding_matrix(K, M_PAR, 8)
+        slab, shards = E.alloc_stripes(len(ids), K, M_PAR, SIZE, dev)
+        originals = {}
+        for b, s in enumerate(ids):
+            for j in range(K):
+                shards[b][j].copy_(torch.from_numpy(splitmix_bytes(SIZE, shard_seed(CFG, s, j))))
+        enc = E.encode_plan(K, M_PAR, Mx, 0).bind([st[:K] for st in shards], [st[K:] for st in shards], SIZE)
+        enc.launch()
+        torch.cuda.synchronize()
+        mine = {}
+        for b, s in enumerate(ids):
+            originals[s] = [t.clone() for t in shards[b]]
+            mine[s] = {"parity": [fnv1a64(t.cpu().numpy()) for t in shards[b][K:]]}
+        # C4's worst-case pattern, batched over this rank's stripes
+        for b in range(len(ids)):
+            for e in ERASED:
+                shards[b][e].zero_()
+        dec = E.DecodePlan(K, M_PAR, Mx, ERASED, 0, 0).bind_stripes(shards, SIZE)
+        dec.launch()
+        torch.cuda.synchronize()
+        for b, s in enumerate(ids):
+            mine[s]["decode_ok"] = all(bool(torch.equal(shards[b][i], originals[s][i])) for i in range(K + M_PAR))
+        # the synchronous drop-in decode (reference semantics) on host buffers
+        s0 = ids[0]
+        host = [originals[s0][i].cpu().numpy().copy() for i in range(K + M_PAR)]
+        for e in DROPIN_ERASED:
+            host[e][:] = 0
+        rc = E.jerasure.jerasure_matrix_decode(K, M_PAR, 8, Mx, 0, DROPIN_ERASED, host[:K], host[K:], SIZE)
+        mine[s0]["dropin_rc"] = rc
+        mine[s0]["dropin_ok"] = all(np.array_equal(host[i], originals[s0][i].cpu().numpy()) for i in range(K + M_PAR))
+        bench.barrier(world)
+        t = bench.max_over_ranks(float(rank + 1), world)
+        gathered = bench.gather(mine, world)
+        import torch.distributed as dist
+        dist.destroy_process_group()
+        q.put((rank, t, gathered, None))
+    except BaseException as ex:  # report, never hang the parent
+        q.put((rank, None, None, repr(ex)))
+        raise
+
+
+def test_two_ranks_code_their_stripes_with_the_library(gpu):
+    import torch.multiprocessing as mp
+
+    from ecdata import fnv1a64, shard_seed, splitmix_bytes
+    from oracle.oracle import Restatement, alloc_shards
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, t, gathered, err in results:
+        assert err is None, f"rank {rank}: {err}"
+        assert t == float(world)
+    for p in procs:
+        assert p.exitcode == 0
+    gathered = results[0][2]
+    merged = {}
+    for part in gathered:
+        assert not (set(part) & set(merged)), "a stripe was coded by two ranks"
+        merged.update(part)
+    assert sorted(merged) == list(range(TOTAL))
+    o = Restatement()
+    Mx = o.vandermonde_coding_matrix(K, M_PAR)
+    for s in range(TOTAL):
+        data = alloc_shards(K, SIZE)
+        for j in range(K):
+            data[j][:SIZE] = splitmix_bytes(SIZE, shard_seed(CFG, s, j))
+        coding = alloc_shards(M_PAR, SIZE)
+        o.matrix_encode(K, M_PAR, Mx, data, coding, SIZE)
+        assert merged[s]["parity"] == [fnv1a64(c[:SIZE]) for c in coding], s
+        assert merged[s]["decode_ok"], s
+    for s in (0, 1):  # each rank's first stripe went through the drop-in decode
+        assert merged[s]["dropin_rc"] == 0 and merged[s]["dropin_ok"], s
+
+
+def _bench(args, env_extra=None, timeout=180):
+    env = dict(os.environ)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=ROOT)
+
+
+def _line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_gpus2_rehearsal_spawns_two_ranks(gpu):
+    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--stripes", "4", "--cpu-seconds", "0",
+                "--no-configs"], {"ECGPU_BENCH_ONE_DEVICE": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["rehearsal"] is True
+    assert [p["rank"] for p in d["per_rank"]] == [0, 1]
+    assert all(p["parity_ok"] for p in d["per_rank"])
+    assert [p["stripe_ids"] for p in d["per_rank"]] == [[0, 6, 4], [1, 7, 4]]  # round-robin global ids
+    assert d["selfcheck_parity_ok"] is True
+
+
+def test_bench_gpus_beyond_visible_devices_fails(gpu):
+    import torch
+    n = torch.cuda.device_count()
+    r = _bench(["--gpus", str(n + 1), "--steps", "1", "--warmup", "0", "--cpu-seconds", "0"], timeout=60)
+    assert r.returncode != 0
+    assert "visible GPUs" in r.stderr
+
+
+def test_bench_config_c5(gpu):
+    r = _bench(["--config", "C5", "--stripes", "2", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0",
+                "--no-configs"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["config"]["workload"].startswith("C5: RS(12,4)")
+    assert (d["config"]["k"], d["config"]["m"], d["config"]["shard_bytes"]) == (12, 4, 16 << 20)
+    assert d["decode_kernel"] is None and d["selfcheck_parity_ok"] is True

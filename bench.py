@@ -609,9 +609,9 @@ def main(argv=None):
             configs = config_block(E, N, dev, stream, kind, bool(args.nt), main_entries)
 
     workload = C["workload"].format(B=B)
+    cpu_ok = None
     if rank == 0:
         cpu = cpu_all = cpu_o3 = None
-        cpu_ok = None
         if host_stripe is not None:
             cpu, cpu_ok = cpu_baseline(args.cpu_seconds, host_stripe, k, m, erasures)
             cpu_all, ok_all = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_stripe, k, m, erasures,

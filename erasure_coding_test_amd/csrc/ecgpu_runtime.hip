@@ -505,13 +505,19 @@ struct PlanKey {
   bool operator==(const PlanKey& o) const { return rows == o.rows && nsrc == o.nsrc && w == o.w && coef == o.coef; }
 };
 
+constexpr size_t kRingBytes = size_t(4) << 20;  // per slot of the pinned copy ring (large calls)
+
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
   uint8_t* stage = nullptr;
   size_t stage_cap = 0;
-  uint8_t* bounce = nullptr;  // pinned host mirror of the staging slab (small calls, see execute)
+  uint8_t* bounce = nullptr;  // pinned host mirror of the staging slab (mid-size calls, see execute)
   size_t bounce_cap = 0;
+  uint8_t* zc = nullptr;      // coherent pinned memory the kernel reads / writes in place (small calls)
+  size_t zc_cap = 0;
+  uint8_t* ring[2] = {nullptr, nullptr};  // pinned two-slot ring of the large-call copy pipelines
+  hipEvent_t ring_ev[2] = {nullptr, nullptr};
   std::list<std::pair<PlanKey, ecgpu_plan*>> plans;  // LRU, front = newest
 };
 
@@ -593,15 +599,42 @@ int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int 
   return ECGPU_OK;
 }
 
-// Small synchronous calls on host buffers: every pageable hipMemcpyAsync
-// pays a fixed staging cost (~10 us each, six of them for RS(4,2)), so up to
-// kBounceMax staged bytes the host side is copied by the CPU through one
-// pinned mirror of the staging slab and crosses PCIe as ONE H2D DMA (inputs)
-// plus one D2H DMA per output.  Above it HIP's pipelined pageable copies win.
+// How a synchronous call moves host (pageable or pinned) buffers, by the
+// bytes it stages (measured on MI355X, tools/hip_overheads.cpp,
+// tools/zero_copy_probe.cpp): every DMA costs ~10 us of setup and a launch +
+// sync ~11 us, so
+//   * up to zc_max() staged bytes: NO DMA.  The calling thread copies the
+//     host side into coherent pinned memory and the kernel reads its sources
+//     and writes its outputs there directly over PCIe (zero-copy; reads and
+//     writes travel opposite directions of the link): one launch per call.
+//   * up to bounce_max(): the host side is copied by the CPU through a pinned
+//     mirror of the staging slab and crosses PCIe as one H2D DMA plus one D2H
+//     DMA per run of adjacent outputs.
+//   * above: sources that are one contiguous run (the client's stripe buffer,
+//     client_main.cpp:1619-1647) or pinned go by direct DMA (a pageable
+//     6 MiB copy runs at the pinned rate); scattered pageable shards, and the
+//     outputs, go through a two-slot pinned ring -- the calling thread fills
+//     (empties) one slot while the DMA engine drains (fills) the other, one
+//     2-D DMA per chunk across all shards.
 constexpr size_t kBounceMax = size_t(2) << 20;
 
 size_t bounce_max() {
   static const size_t v = size_t(env_int("ECGPU_BOUNCE_KIB", int(kBounceMax >> 10))) << 10;
+  return v;
+}
+
+size_t zc_max() {
+  static const size_t v = size_t(env_int("ECGPU_ZC_KIB", 1024)) << 10;
+  return v;
+}
+
+bool inline_enabled() {
+  static const bool v = env_int("ECGPU_INLINE", 1) != 0;
+  return v;
+}
+
+bool ring_enabled() {
+  static const bool v = env_int("ECGPU_RING", 1) != 0;
   return v;
 }
 
@@ -613,6 +646,31 @@ int ensure_bounce(Ctx* c, size_t bytes) {
   c->bounce_cap = 0;
   ECGPU_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->bounce), bytes, hipHostMallocDefault));
   c->bounce_cap = bytes;
+  return ECGPU_OK;
+}
+
+// Coherent (fine-grained) pinned memory: the GPU does not cache it, so CPU
+// writes before a launch and GPU writes before its completion are visible to
+// the other side without cache maintenance.  Grows geometrically.
+int ensure_zc(Ctx* c, size_t bytes) {
+  if (bytes <= c->zc_cap) return ECGPU_OK;
+  DeviceGuard g(c->device);
+  if (c->zc) ECGPU_HIP(hipHostFree(c->zc));
+  c->zc = nullptr;
+  c->zc_cap = 0;
+  const size_t want = std::max(bytes, size_t(256) << 10);
+  ECGPU_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->zc), want, hipHostMallocMapped | hipHostMallocCoherent));
+  c->zc_cap = want;
+  return ECGPU_OK;
+}
+
+int ensure_ring(Ctx* c) {
+  if (c->ring[0]) return ECGPU_OK;
+  DeviceGuard g(c->device);
+  for (int i = 0; i < 2; ++i) {
+    ECGPU_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->ring[i]), kRingBytes, hipHostMallocDefault));
+    ECGPU_HIP(hipEventCreateWithFlags(&c->ring_ev[i], hipEventDisableTiming));
+  }
   return ECGPU_OK;
 }
 
@@ -648,6 +706,15 @@ int classify(const void* p, int device, bool* on_device) {
   return ECGPU_OK;
 }
 
+bool is_pinned(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
 // ------------------------------------------------------ stats counters ----
 std::mutex g_stats_mu;
 double g_stats[3] = {0, 0, 0};  // xor, gf, memcpy -- jerasure.cpp:1145-1147 order
@@ -675,22 +742,15 @@ int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>&
     // pageable 2-D copy with gaps between rows ran 15x slower than per-shard
     // copies (RS(6,3) 1 MiB, shards malloc'd one by one, 16 B apart)
     bool ok = two_d && pitch > 0 && size_t(pitch) >= bytes;
-    if (ok && size_t(pitch) != bytes) {
-      hipPointerAttribute_t attr;
-      if (hipPointerGetAttributes(&attr, hp[a]) != hipSuccess) {
-        (void)hipGetLastError();
-        ok = false;
-      } else {
-        ok = attr.type == hipMemoryTypeHost;  // pinned or registered
-      }
-    }
+    if (ok && size_t(pitch) != bytes) ok = is_pinned(hp[a]);  // pinned or registered
     if (ok)
       while (b < n && hp[b] - hp[b - 1] == pitch) ++b;
+    // a gapped run must be pinned at both ends (one registration or
+    // allocation spans it; HIP rejects a span across separately registered
+    // buffers at enqueue, which falls back below)
+    if (b - a >= 2 && size_t(pitch) != bytes && !is_pinned(hp[b - 1] + bytes - 1)) b = a + 1;
     uint8_t* d = d0 + a * dstride;
     if (b - a >= 2) {
-      // HIP rejects (at enqueue) a 2-D copy whose host span crosses
-      // allocations it knows separately, e.g. shards registered one by one:
-      // those go shard by shard below
       const hipError_t e =
           h2d ? hipMemcpy2DAsync(d, dstride, hp[a], size_t(pitch), bytes, b - a, hipMemcpyHostToDevice, s)
               : hipMemcpy2DAsync(hp[a], size_t(pitch), d, dstride, bytes, b - a, hipMemcpyDeviceToHost, s);
@@ -698,7 +758,7 @@ int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>&
         a = b;
         continue;
       }
-      if (e != hipErrorInvalidValue) return fail(ECGPU_ERR_HIP, std::string("hipMemcpy2DAsync: ") + hipGetErrorString(e));
+      // not enqueued: fall back to one copy per shard (the error is not sticky)
       (void)hipGetLastError();
     }
     for (size_t i = a; i < b; ++i) {
@@ -712,6 +772,129 @@ int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>&
   return ECGPU_OK;
 }
 
+// Chunk length of the ring pipelines: one slot holds one chunk of every
+// shard (4 KiB multiples), so one 2-D DMA moves a chunk of all n shards.
+size_t ring_chunk(size_t n, size_t bytes) {
+  size_t len = (kRingBytes / std::max<size_t>(n, 1)) & ~size_t(4095);
+  if (len == 0) len = kRingBytes / std::max<size_t>(n, 1);
+  return std::max<size_t>(1, std::min(len, bytes));
+}
+
+// Sources host -> device slots d0 + i * dstride.  Pinned shards and one
+// contiguous pageable run go by direct DMA (copy_shards); scattered pageable
+// shards are packed chunk by chunk into the pinned ring by this thread while
+// the DMA engine drains the other slot.
+int stage_in(Ctx* c, uint8_t* d0, size_t dstride, const std::vector<char*>& hp, size_t bytes) {
+  const size_t n = hp.size();
+  if (n == 0) return ECGPU_OK;
+  bool contiguous = n >= 2;
+  for (size_t i = 1; i < n && contiguous; ++i) contiguous = hp[i] == hp[0] + i * bytes;
+  bool pinned = true;
+  for (size_t i = 0; i < n && pinned; ++i) pinned = is_pinned(hp[i]);
+  if (contiguous || pinned || !ring_enabled()) return copy_shards(true, d0, dstride, hp, bytes, c->stream);
+  if (int rc = ensure_ring(c)) return rc;
+  const size_t len = ring_chunk(n, bytes);
+  for (size_t off = 0, ch = 0; off < bytes; off += len, ++ch) {
+    const int sl = int(ch & 1);
+    const size_t l = std::min(len, bytes - off);
+    if (ch >= 2) ECGPU_HIP(hipEventSynchronize(c->ring_ev[sl]));  // the DMA that last read this slot is done
+    for (size_t i = 0; i < n; ++i) std::memcpy(c->ring[sl] + i * l, hp[i] + off, l);
+    ECGPU_HIP(hipMemcpy2DAsync(d0 + off, dstride, c->ring[sl], l, l, n, hipMemcpyHostToDevice, c->stream));
+    ECGPU_HIP(hipEventRecord(c->ring_ev[sl], c->stream));
+  }
+  return ECGPU_OK;
+}
+
+// Outputs device slots d0 + i * dstride -> host hp[i], after the work queued
+// on the stream.  Pinned outputs and one contiguous pageable run go by direct
+// DMA; the rest through the pinned ring: the DMA engine fills one slot while
+// this thread copies the other out.  Returns once every byte is in place.
+int stage_out(Ctx* c, uint8_t* d0, size_t dstride, const std::vector<char*>& hp, size_t bytes) {
+  const size_t n = hp.size();
+  if (n == 0) return ECGPU_OK;
+  bool contiguous = n >= 2;
+  for (size_t i = 1; i < n && contiguous; ++i) contiguous = hp[i] == hp[0] + i * bytes;
+  bool pinned = true;
+  for (size_t i = 0; i < n && pinned; ++i) pinned = is_pinned(hp[i]);
+  if (contiguous || pinned || !ring_enabled()) {
+    if (int rc = copy_shards(false, d0, dstride, hp, bytes, c->stream)) return rc;
+    ECGPU_HIP(hipStreamSynchronize(c->stream));
+    return ECGPU_OK;
+  }
+  if (int rc = ensure_ring(c)) return rc;
+  const size_t len = ring_chunk(n, bytes);
+  const size_t nch = (bytes + len - 1) / len;
+  auto enqueue = [&](size_t ch) -> int {
+    const int sl = int(ch & 1);
+    const size_t off = ch * len, l = std::min(len, bytes - off);
+    ECGPU_HIP(hipMemcpy2DAsync(c->ring[sl], l, d0 + off, dstride, l, n, hipMemcpyDeviceToHost, c->stream));
+    ECGPU_HIP(hipEventRecord(c->ring_ev[sl], c->stream));
+    return ECGPU_OK;
+  };
+  for (size_t ch = 0; ch < std::min<size_t>(2, nch); ++ch)
+    if (int rc = enqueue(ch)) return rc;
+  for (size_t ch = 0; ch < nch; ++ch) {
+    const int sl = int(ch & 1);
+    const size_t off = ch * len, l = std::min(len, bytes - off);
+    ECGPU_HIP(hipEventSynchronize(c->ring_ev[sl]));
+    for (size_t i = 0; i < n; ++i) std::memcpy(hp[i] + off, c->ring[sl] + i * l, l);
+    if (ch + 2 < nch)
+      if (int rc = enqueue(ch + 2)) return rc;
+  }
+  ECGPU_HIP(hipStreamSynchronize(c->stream));
+  return ECGPU_OK;
+}
+
+// P3 tables of one coefficient (see build_tables).
+void build_p3(uint32_t c, uint32_t* p3) {
+  const auto& T = gf8().mul[c & 0xFF];
+  for (int i = 0; i < dev::kP3Words; ++i) p3[i] = 0;
+  for (int e = 0; e < 8; ++e) {
+    p3[e >> 2] |= uint32_t(T[e]) << (8 * (e & 3));
+    p3[2 + (e >> 2)] |= uint32_t(T[e << 3]) << (8 * (e & 3));
+  }
+  for (int e = 0; e < 4; ++e) p3[4] |= uint32_t(T[e << 6]) << (8 * e);
+}
+
+// Can a fused op run as gf_apply_inl launches (everything in the kernel
+// arguments, no table or pointer upload)?  w = 8, 1..16 sources, the
+// production engine, and no output that is also a source when the rows need
+// more than one launch.
+bool inline_ok(const FusedOp& op) {
+  const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
+  return inline_enabled() && op.w == 8 && nsrc >= 1 && nsrc <= dev::kMaxSpecK && rows >= 1 &&
+         env_int("ECGPU_KERNEL", ECGPU_KERNEL_PERM) == ECGPU_KERNEL_PERM && !(op.dst_is_src && rows > dev::kMaxRows);
+}
+
+// One gf_apply_inl launch per <= 4 output rows over `size` bytes.
+int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, const std::vector<uint8_t*>& dp,
+                  int64_t size, hipStream_t s) {
+  const int K = int(sp.size()), rows = int(dp.size());
+  bool aligned = true;
+  for (auto* p : sp) aligned &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  for (auto* p : dp) aligned &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  const int64_t nvec = aligned ? size / 16 : 0, byte0 = nvec * 16;
+  const int64_t nbv = (nvec + dev::kBlock - 1) / dev::kBlock;
+  const int64_t nbb = (size - byte0 + dev::kBlock - 1) / dev::kBlock;
+  for (int r0 = 0; r0 < rows; r0 += dev::kMaxRows) {
+    const int R = std::min(dev::kMaxRows, rows - r0);
+    const InlineKernelFn fn = inline_kernel(K, R, unit_variant(op.coef, K, r0, R));
+    if (!fn) return fail(ECGPU_ERR, "no inline kernel for K = " + std::to_string(K));
+    dev::InlineArgs a{};
+    for (int j = 0; j < K; ++j) a.src[j] = sp[size_t(j)];
+    for (int r = 0; r < R; ++r) a.dst[r] = dp[size_t(r0 + r)];
+    a.nvec = nvec;
+    a.size = size;
+    a.byte0 = byte0;
+    a.nblk_vec = int(nbv);
+    for (int r = 0; r < R; ++r)
+      for (int j = 0; j < K; ++j) build_p3(op.coef[size_t(r0 + r) * K + j], &a.ptab[(r * K + j) * dev::kP3Words]);
+    void* args[] = {&a};
+    ECGPU_HIP(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(unsigned(nbv + nbb)), dim3(dev::kBlock), args,
+                              0, s));
+  }
+  return ECGPU_OK;
+}
 
 // Runs a fused op synchronously over `size` bytes of every buffer.
 int execute(const FusedOp& op, int64_t size) {
@@ -745,6 +928,30 @@ int execute(const FusedOp& op, int64_t size) {
     }
   }
   const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
+  auto buf_index = [&](void* p) { return size_t(std::find(bufs.begin(), bufs.end(), p) - bufs.begin()); };
+  const bool inl = inline_ok(op);
+
+  // --- small calls: zero-copy through coherent pinned memory, one launch ---
+  if (inl && nstage > 0 && nstage * size_t(size) <= zc_max()) {
+    if (int rc = ensure_zc(c, nstage * slot)) return rc;
+    size_t next = 0;
+    for (size_t i = 0; i < bufs.size(); ++i)
+      if (staged[i]) devp[i] = c->zc + (next++) * slot;
+    for (int j = 0; j < nsrc; ++j)
+      if (staged[size_t(j)]) std::memcpy(devp[size_t(j)], op.srcs[size_t(j)], size_t(size));
+    std::vector<const uint8_t*> sp(devp.begin(), devp.begin() + nsrc);
+    std::vector<uint8_t*> dp(static_cast<size_t>(rows));
+    for (int r = 0; r < rows; ++r) dp[size_t(r)] = devp[buf_index(op.dsts[size_t(r)])];
+    if (int rc = launch_inline(op, sp, dp, size, c->stream)) return rc;
+    ECGPU_HIP(hipStreamSynchronize(c->stream));
+    ECGPU_HIP(hipGetLastError());
+    for (int r = 0; r < rows; ++r) {
+      const size_t i = buf_index(op.dsts[size_t(r)]);
+      if (staged[i]) std::memcpy(op.dsts[size_t(r)], devp[i], size_t(size));
+    }
+    return ECGPU_OK;
+  }
+
   // With several launches (> 4 rows) an output that is also a source must
   // not be overwritten before the last launch reads it: write to temps.
   const bool via_temp = op.dst_is_src && rows > dev::kMaxRows;
@@ -759,8 +966,6 @@ int execute(const FusedOp& op, int64_t size) {
   const bool bounce = nstage > 0 && nstage * slot <= bounce_max();
   if (bounce && (rc = ensure_bounce(c, nstage * slot)) != ECGPU_OK) return rc;
   auto bounce_of = [&](size_t i) { return c->bounce + (devp[i] - c->stage); };
-  // staged sources occupy slots 0, 1, ... in order: from a stripe buffer
-  // (the client's data shards, client_main.cpp:1619-1647) ONE 2-D copy
   std::vector<char*> staged_hp;
   for (size_t j = 0; j < op.srcs.size(); ++j)
     if (staged[j]) {
@@ -769,20 +974,20 @@ int execute(const FusedOp& op, int64_t size) {
     }
   if (bounce && !staged_hp.empty())
     ECGPU_HIP(hipMemcpyAsync(c->stage, c->bounce, staged_hp.size() * slot, hipMemcpyHostToDevice, c->stream));
-  else if ((rc = copy_shards(true, c->stage, slot, staged_hp, size_t(size), c->stream)) != ECGPU_OK)
+  else if ((rc = stage_in(c, c->stage, slot, staged_hp, size_t(size))) != ECGPU_OK)
     return rc;
 
   std::vector<const uint8_t*> sp(static_cast<size_t>(nsrc));
   std::vector<uint8_t*> dp(static_cast<size_t>(rows));
   for (int j = 0; j < nsrc; ++j) sp[j] = devp[j];
-  for (int r = 0; r < rows; ++r) {
-    const size_t i = size_t(std::find(bufs.begin(), bufs.end(), op.dsts[r]) - bufs.begin());
-    dp[r] = via_temp ? c->stage + (nstage + size_t(r)) * slot : devp[i];
-  }
+  for (int r = 0; r < rows; ++r)
+    dp[r] = via_temp ? c->stage + (nstage + size_t(r)) * slot : devp[buf_index(op.dsts[size_t(r)])];
   if (nsrc == 0) {
     // Every output is identically zero (e.g. region multiply by 0 without
     // add, galois.cpp:447-451): nothing to read.
     for (int r = 0; r < rows; ++r) ECGPU_HIP(hipMemsetAsync(dp[r], 0, size_t(size), c->stream));
+  } else if (inl) {
+    if ((rc = launch_inline(op, sp, dp, size, c->stream)) != ECGPU_OK) return rc;
   } else {
     ecgpu_plan* p = nullptr;
     rc = ctx_plan(c, rows, nsrc, op.coef, op.w, &p);
@@ -792,38 +997,43 @@ int execute(const FusedOp& op, int64_t size) {
     rc = plan_launch(p, c->stream);
     if (rc != ECGPU_OK) return rc;
   }
-  std::vector<char*> out_hp;  // staged outputs in consecutive slots: one 2-D copy back
-  uint8_t* out_d0 = nullptr;
-  bool out_run = !bounce;
+  // staged outputs, in slot order
+  std::vector<std::pair<uint8_t*, char*>> outs;  // (device slot, host pointer)
   for (int r = 0; r < rows; ++r) {
-    const size_t i = size_t(std::find(bufs.begin(), bufs.end(), op.dsts[r]) - bufs.begin());
+    const size_t i = buf_index(op.dsts[size_t(r)]);
     if (via_temp)
       ECGPU_HIP(hipMemcpyAsync(devp[i], dp[r], size_t(size), hipMemcpyDeviceToDevice, c->stream));
-    if (!staged[i]) continue;
-    if (bounce) {
-      ECGPU_HIP(hipMemcpyAsync(bounce_of(i), devp[i], size_t(size), hipMemcpyDeviceToHost, c->stream));
-      continue;
-    }
-    if (out_hp.empty()) out_d0 = devp[i];
-    out_run &= devp[i] == out_d0 + out_hp.size() * slot;
-    out_hp.push_back(static_cast<char*>(op.dsts[r]));
+    if (staged[i]) outs.emplace_back(devp[i], static_cast<char*>(op.dsts[size_t(r)]));
   }
-  if (out_run) {
-    if ((rc = copy_shards(false, out_d0, slot, out_hp, size_t(size), c->stream)) != ECGPU_OK) return rc;
-  } else {
-    for (int r = 0; r < rows; ++r) {
-      const size_t i = size_t(std::find(bufs.begin(), bufs.end(), op.dsts[r]) - bufs.begin());
-      if (staged[i] && !bounce)
-        ECGPU_HIP(hipMemcpyAsync(op.dsts[r], devp[i], size_t(size), hipMemcpyDeviceToHost, c->stream));
+  std::sort(outs.begin(), outs.end());
+  if (bounce) {
+    // one D2H per run of adjacent slots (the bounce mirrors the slab)
+    for (size_t a = 0; a < outs.size();) {
+      size_t b = a + 1;
+      while (b < outs.size() && outs[b].first == outs[b - 1].first + slot) ++b;
+      const size_t off = size_t(outs[a].first - c->stage);
+      ECGPU_HIP(hipMemcpyAsync(c->bounce + off, outs[a].first, (b - a - 1) * slot + size_t(size),
+                               hipMemcpyDeviceToHost, c->stream));
+      a = b;
     }
+    ECGPU_HIP(hipStreamSynchronize(c->stream));
+    ECGPU_HIP(hipGetLastError());
+    for (const auto& o : outs) std::memcpy(o.second, c->bounce + (o.first - c->stage), size_t(size));
+    return ECGPU_OK;
+  }
+  // outputs in consecutive slots: one ring pipeline (or direct DMA); else one by one
+  bool consecutive = true;
+  for (size_t i = 1; i < outs.size() && consecutive; ++i) consecutive = outs[i].first == outs[0].first + i * slot;
+  if (consecutive && !outs.empty()) {
+    std::vector<char*> hp;
+    for (const auto& o : outs) hp.push_back(o.second);
+    if ((rc = stage_out(c, outs[0].first, slot, hp, size_t(size))) != ECGPU_OK) return rc;
+  } else {
+    for (const auto& o : outs)
+      if ((rc = stage_out(c, o.first, slot, {o.second}, size_t(size))) != ECGPU_OK) return rc;
   }
   ECGPU_HIP(hipStreamSynchronize(c->stream));
   ECGPU_HIP(hipGetLastError());
-  if (bounce)
-    for (int r = 0; r < rows; ++r) {
-      const size_t i = size_t(std::find(bufs.begin(), bufs.end(), op.dsts[r]) - bufs.begin());
-      if (staged[i]) std::memcpy(op.dsts[r], bounce_of(i), size_t(size));
-    }
   return ECGPU_OK;
 }
 

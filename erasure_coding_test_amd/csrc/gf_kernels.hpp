@@ -296,36 +296,44 @@ __device__ __forceinline__ void mac3(Xacc& x, const kconst_u32* __restrict__ t, 
   x.add(__builtin_amdgcn_perm(t[4], t[4], s.s2));
 }
 
+// R output columns from the K source columns of one lane with the
+// 3-bit-slice tables at `ptab` ([R][K][kP3Words], constant address space: a
+// device table or the launch's own kernel arguments, see gf_apply_inl).
+template <int K, int R, int UNITS>
+__device__ __forceinline__ void combine3(const kconst_u32* __restrict__ ptab, const u32x4 (&x)[K], u32x4 (&acc)[R]) {
+  Xacc xa[R][4];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    Sel3 sl[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sl[c] = sel3(x[j][c]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (is_unit<UNITS>(r, j)) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xa[r][c].add(x[j][c]);
+      } else {
+        const kconst_u32* t = ptab + (r * K + j) * kP3Words;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) mac3(xa[r][c], t, sl[c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = xa[r][c].value();
+}
+
 // R output columns from the K source columns of one lane (combine_store:
 // then R stores).  SLICES = 3: production 3-bit-slice tables (ptab); 2: the round-1 2-bit
 // form (qtab), kept for A/B timing in the diagnostic library.
 template <int K, int R, int UNITS, int SLICES>
 __device__ __forceinline__ void combine(const ApplyArgs& a, const u32x4 (&x)[K], u32x4 (&acc)[R]) {
   if constexpr (SLICES == 3) {
-    Xacc xa[R][4];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      Sel3 sl[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) sl[c] = sel3(x[j][c]);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (is_unit<UNITS>(r, j)) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) xa[r][c].add(x[j][c]);
-        } else {
-          // constant address space: always a scalar load, even after an
-          // LDS-DMA (which the compiler otherwise treats as a clobber)
-          const kconst_u32* t = (const kconst_u32*)a.ptab + (r * K + j) * kP3Words;  // C cast: generic -> constant
-#pragma unroll
-          for (int c = 0; c < 4; ++c) mac3(xa[r][c], t, sl[c]);
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[r][c] = xa[r][c].value();
+    // constant address space: always a scalar load, even after an LDS-DMA
+    // (which the compiler otherwise treats as a clobber)
+    combine3<K, R, UNITS>((const kconst_u32*)a.ptab, x, acc);  // C cast: generic -> constant
   } else {
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
@@ -441,6 +449,64 @@ __device__ __forceinline__ void gf_apply_body(const ApplyArgs& a) {
 template <int K, int R, int UNITS, int VEC = 1, int SLICES = 3, int NT = 3>
 __global__ __launch_bounds__(kBlock) void gf_apply(ApplyArgs a) {
   gf_apply_body<K, R, UNITS, VEC, SLICES, NT>(a);
+}
+
+// ---------------------------------------------- one-stripe inline form ----
+// A synchronous one-stripe call (the drop-in jerasure_* / galois_* names)
+// is latency-bound: uploading its pointer table and coefficient tables cost
+// two to five small DMAs (~10 us each on MI355X, tools/hip_overheads.cpp)
+// before the kernel could start.  Here the launch carries everything in its
+// kernel arguments (< 4 KiB): the K source and R destination pointers and
+// the rows' 3-bit-slice tables, read with scalar loads straight from the
+// kernarg segment.  One launch covers the whole shard: blocks below
+// nblk_vec do 16-B columns (the production combine, unit structure UNITS),
+// the blocks after them one byte per lane for the tail [byte0, size) -- or
+// every byte when a pointer is not 16-B aligned (nvec = 0).
+struct InlineArgs {
+  const uint8_t* src[kMaxSpecK];
+  uint8_t* dst[kMaxRows];
+  int64_t nvec, size, byte0;
+  int nblk_vec;
+  int pad_;
+  uint32_t ptab[kMaxRows * kMaxSpecK * kP3Words];  // [R][K][kP3Words], this launch's rows
+};
+static_assert(sizeof(InlineArgs) <= 4096, "kernel arguments are limited to 4 KiB");
+
+template <int K, int R, int UNITS>
+__global__ __launch_bounds__(kBlock) void gf_apply_inl(InlineArgs a) {
+  const kconst_u32* ptab = (const kconst_u32*)a.ptab;  // kernarg segment: scalar loads
+  if (int(blockIdx.x) < a.nblk_vec) {
+    const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (col >= a.nvec) return;
+    uint8_t* dp[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) dp[r] = a.dst[r];
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = load16t<1>(a.src[j], col);
+    u32x4 acc[R];
+    combine3<K, R, UNITS>(ptab, x, acc);
+#pragma unroll
+    for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
+    return;
+  }
+  const int64_t x = a.byte0 + int64_t(int(blockIdx.x) - a.nblk_vec) * kBlock + threadIdx.x;
+  if (x >= a.size) return;
+  Xacc xa[R];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t v = a.src[j][x];
+    const Sel3 sl = sel3(v);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (is_unit<UNITS>(r, j))
+        xa[r].add(v);
+      else
+        mac3(xa[r], ptab + (r * K + j) * kP3Words, sl);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) a.dst[r][x] = uint8_t(xa[r].value());
 }
 
 // LDS-DMA form: the K source columns of a lane arrive by

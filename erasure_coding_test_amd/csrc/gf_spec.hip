@@ -26,8 +26,13 @@ struct Pol {
                                             apply_fn<K, 3, S>(), apply_fn<K, 4, S>()};
 };
 
+template <int K, int U>
+constexpr InlineKernelFn inl_fn() { return &dev::gf_apply_inl<K, kR, kUnitVariants[U]>; }
+
 template <int K>
 struct Row {
+  static constexpr InlineKernelFn inl[5] = {inl_fn<K, 0>(), inl_fn<K, 1>(), inl_fn<K, 2>(), inl_fn<K, 3>(),
+                                            inl_fn<K, 4>()};
   static constexpr const SpecKernelFn* apply[kStorePolicies] = {Pol<K, 0>::apply, Pol<K, 1>::apply};
   static constexpr SpecKernelFn lds = &dev::gf_apply_lds<K, kR>;
 };
@@ -39,6 +44,13 @@ SpecKernelFn pick(bool lds, int K, int u, int store_pol) {
   return out;
 }
 
+template <int... Ks>
+InlineKernelFn pick_inl(int K, int u) {
+  InlineKernelFn out = nullptr;
+  ((K == Ks ? (out = Row<Ks>::inl[u], 0) : 0), ...);
+  return out;
+}
+
 }  // namespace
 
 #define ECGPU_CAT2(a, b) a##b
@@ -46,6 +58,11 @@ SpecKernelFn pick(bool lds, int K, int u, int store_pol) {
 SpecKernelFn ECGPU_CAT(spec_kernel_r, ECGPU_SPEC_R)(bool lds, int K, int unit_variant, int store_pol) {
   if (unit_variant < 0 || unit_variant > 4 || store_pol < 0 || store_pol >= kStorePolicies) return nullptr;
   return pick<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>(lds, K, unit_variant, store_pol);
+}
+
+InlineKernelFn ECGPU_CAT(inline_kernel_r, ECGPU_SPEC_R)(int K, int unit_variant) {
+  if (unit_variant < 0 || unit_variant > 4) return nullptr;
+  return pick_inl<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>(K, unit_variant);
 }
 
 }  // namespace ecgpu

@@ -9,6 +9,7 @@
 namespace ecgpu {
 
 using SpecKernelFn = void (*)(dev::ApplyArgs);
+using InlineKernelFn = void (*)(dev::InlineArgs);
 constexpr int kStorePolicies = 2;
 
 // store_pol: store cache policy of the production kernel, 0 plain, 1 nt
@@ -20,6 +21,23 @@ SpecKernelFn spec_kernel_r1(bool lds, int K, int unit_variant, int store_pol);
 SpecKernelFn spec_kernel_r2(bool lds, int K, int unit_variant, int store_pol);
 SpecKernelFn spec_kernel_r3(bool lds, int K, int unit_variant, int store_pol);
 SpecKernelFn spec_kernel_r4(bool lds, int K, int unit_variant, int store_pol);
+
+// gf_apply_inl<K, R, UNITS> (one stripe, everything in the kernel
+// arguments); nullptr if K is outside 1..kMaxSpecK.
+InlineKernelFn inline_kernel_r1(int K, int unit_variant);
+InlineKernelFn inline_kernel_r2(int K, int unit_variant);
+InlineKernelFn inline_kernel_r3(int K, int unit_variant);
+InlineKernelFn inline_kernel_r4(int K, int unit_variant);
+
+inline InlineKernelFn inline_kernel(int K, int R, int unit_variant) {
+  switch (R) {
+    case 1: return inline_kernel_r1(K, unit_variant);
+    case 2: return inline_kernel_r2(K, unit_variant);
+    case 3: return inline_kernel_r3(K, unit_variant);
+    case 4: return inline_kernel_r4(K, unit_variant);
+    default: return nullptr;
+  }
+}
 
 inline SpecKernelFn spec_kernel(bool lds, int K, int R, int unit_variant, int store_pol) {
   switch (R) {

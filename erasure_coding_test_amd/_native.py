@@ -111,6 +111,8 @@ SIGNATURES = {
     "ecgpu_host_unregister": (c_int, [c_void_p]),
     "ecgpu_accum_create": (c_void_p, [c_int, c_int64, c_int]),
     "ecgpu_accum_add": (c_int, [c_void_p, c_void_p, c_int_p]),
+    "ecgpu_accum_add_async": (c_int, [c_void_p, c_void_p, c_int_p]),
+    "ecgpu_accum_sync": (c_int, [c_void_p]),
     "ecgpu_accum_read": (c_int, [c_void_p, c_int, c_void_p, c_int64]),
     "ecgpu_accum_device_ptr": (c_void_p, [c_void_p, c_int]),
     "ecgpu_accum_reset": (c_int, [c_void_p]),
@@ -142,6 +144,8 @@ def int_array(values) -> ctypes.Array:
     """C int[] from ints (values wrap to 32 bits like a C int assignment:
     w = 32 coefficients >= 2^31 pass through).  Long inputs -- bit-matrices,
     k*m*w*w ints -- convert through numpy (2.5x faster at 2,560 entries)."""
+    if not isinstance(values, np.ndarray) and not hasattr(values, "__len__"):
+        values = list(values)  # generators and other unsized iterables
     if isinstance(values, np.ndarray) or len(values) >= 64:
         a = np.asarray(values)
         if a.dtype.kind not in "iu":

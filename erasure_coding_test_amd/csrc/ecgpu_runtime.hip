@@ -15,14 +15,18 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <list>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -505,8 +509,6 @@ struct PlanKey {
   bool operator==(const PlanKey& o) const { return rows == o.rows && nsrc == o.nsrc && w == o.w && coef == o.coef; }
 };
 
-constexpr size_t kRingBytes = size_t(4) << 20;  // per slot of the pinned copy ring (large calls)
-
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
@@ -516,8 +518,6 @@ struct Ctx {
   size_t bounce_cap = 0;
   uint8_t* zc = nullptr;      // coherent pinned memory the kernel reads / writes in place (small calls)
   size_t zc_cap = 0;
-  uint8_t* ring[2] = {nullptr, nullptr};  // pinned two-slot ring of the large-call copy pipelines
-  hipEvent_t ring_ev[2] = {nullptr, nullptr};
   std::list<std::pair<PlanKey, ecgpu_plan*>> plans;  // LRU, front = newest
 };
 
@@ -601,8 +601,8 @@ int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int 
 
 // How a synchronous call moves host (pageable or pinned) buffers, by the
 // bytes it stages (measured on MI355X, tools/hip_overheads.cpp,
-// tools/zero_copy_probe.cpp): every DMA costs ~10 us of setup and a launch +
-// sync ~11 us, so
+// tools/zero_copy_probe.cpp): every DMA costs ~10 us of setup
+// and a launch + sync ~11 us, so
 //   * up to zc_max() staged bytes: NO DMA.  The calling thread copies the
 //     host side into coherent pinned memory and the kernel reads its sources
 //     and writes its outputs there directly over PCIe (zero-copy; reads and
@@ -610,12 +610,11 @@ int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int 
 //   * up to bounce_max(): the host side is copied by the CPU through a pinned
 //     mirror of the staging slab and crosses PCIe as one H2D DMA plus one D2H
 //     DMA per run of adjacent outputs.
-//   * above: sources that are one contiguous run (the client's stripe buffer,
-//     client_main.cpp:1619-1647) or pinned go by direct DMA (a pageable
-//     6 MiB copy runs at the pinned rate); scattered pageable shards, and the
-//     outputs, go through a two-slot pinned ring -- the calling thread fills
-//     (empties) one slot while the DMA engine drains (fills) the other, one
-//     2-D DMA per chunk across all shards.
+//   * above: HIP's own pageable copies (a 6 MiB pageable DMA runs at the
+//     pinned rate, 120 us), one 2-D copy per run of evenly spaced shards
+//     (copy_shards).  Staging large calls through a pinned ring filled by
+//     this thread instead lost 10-40 % (a single thread copies cold memory at
+//     ~35 GB/s, below the link; profiles/r02_dropin_ab.txt).
 constexpr size_t kBounceMax = size_t(2) << 20;
 
 size_t bounce_max() {
@@ -630,11 +629,6 @@ size_t zc_max() {
 
 bool inline_enabled() {
   static const bool v = env_int("ECGPU_INLINE", 1) != 0;
-  return v;
-}
-
-bool ring_enabled() {
-  static const bool v = env_int("ECGPU_RING", 1) != 0;
   return v;
 }
 
@@ -661,16 +655,6 @@ int ensure_zc(Ctx* c, size_t bytes) {
   const size_t want = std::max(bytes, size_t(256) << 10);
   ECGPU_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->zc), want, hipHostMallocMapped | hipHostMallocCoherent));
   c->zc_cap = want;
-  return ECGPU_OK;
-}
-
-int ensure_ring(Ctx* c) {
-  if (c->ring[0]) return ECGPU_OK;
-  DeviceGuard g(c->device);
-  for (int i = 0; i < 2; ++i) {
-    ECGPU_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->ring[i]), kRingBytes, hipHostMallocDefault));
-    ECGPU_HIP(hipEventCreateWithFlags(&c->ring_ev[i], hipEventDisableTiming));
-  }
   return ECGPU_OK;
 }
 
@@ -769,79 +753,6 @@ int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>&
     }
     a = b;
   }
-  return ECGPU_OK;
-}
-
-// Chunk length of the ring pipelines: one slot holds one chunk of every
-// shard (4 KiB multiples), so one 2-D DMA moves a chunk of all n shards.
-size_t ring_chunk(size_t n, size_t bytes) {
-  size_t len = (kRingBytes / std::max<size_t>(n, 1)) & ~size_t(4095);
-  if (len == 0) len = kRingBytes / std::max<size_t>(n, 1);
-  return std::max<size_t>(1, std::min(len, bytes));
-}
-
-// Sources host -> device slots d0 + i * dstride.  Pinned shards and one
-// contiguous pageable run go by direct DMA (copy_shards); scattered pageable
-// shards are packed chunk by chunk into the pinned ring by this thread while
-// the DMA engine drains the other slot.
-int stage_in(Ctx* c, uint8_t* d0, size_t dstride, const std::vector<char*>& hp, size_t bytes) {
-  const size_t n = hp.size();
-  if (n == 0) return ECGPU_OK;
-  bool contiguous = n >= 2;
-  for (size_t i = 1; i < n && contiguous; ++i) contiguous = hp[i] == hp[0] + i * bytes;
-  bool pinned = true;
-  for (size_t i = 0; i < n && pinned; ++i) pinned = is_pinned(hp[i]);
-  if (contiguous || pinned || !ring_enabled()) return copy_shards(true, d0, dstride, hp, bytes, c->stream);
-  if (int rc = ensure_ring(c)) return rc;
-  const size_t len = ring_chunk(n, bytes);
-  for (size_t off = 0, ch = 0; off < bytes; off += len, ++ch) {
-    const int sl = int(ch & 1);
-    const size_t l = std::min(len, bytes - off);
-    if (ch >= 2) ECGPU_HIP(hipEventSynchronize(c->ring_ev[sl]));  // the DMA that last read this slot is done
-    for (size_t i = 0; i < n; ++i) std::memcpy(c->ring[sl] + i * l, hp[i] + off, l);
-    ECGPU_HIP(hipMemcpy2DAsync(d0 + off, dstride, c->ring[sl], l, l, n, hipMemcpyHostToDevice, c->stream));
-    ECGPU_HIP(hipEventRecord(c->ring_ev[sl], c->stream));
-  }
-  return ECGPU_OK;
-}
-
-// Outputs device slots d0 + i * dstride -> host hp[i], after the work queued
-// on the stream.  Pinned outputs and one contiguous pageable run go by direct
-// DMA; the rest through the pinned ring: the DMA engine fills one slot while
-// this thread copies the other out.  Returns once every byte is in place.
-int stage_out(Ctx* c, uint8_t* d0, size_t dstride, const std::vector<char*>& hp, size_t bytes) {
-  const size_t n = hp.size();
-  if (n == 0) return ECGPU_OK;
-  bool contiguous = n >= 2;
-  for (size_t i = 1; i < n && contiguous; ++i) contiguous = hp[i] == hp[0] + i * bytes;
-  bool pinned = true;
-  for (size_t i = 0; i < n && pinned; ++i) pinned = is_pinned(hp[i]);
-  if (contiguous || pinned || !ring_enabled()) {
-    if (int rc = copy_shards(false, d0, dstride, hp, bytes, c->stream)) return rc;
-    ECGPU_HIP(hipStreamSynchronize(c->stream));
-    return ECGPU_OK;
-  }
-  if (int rc = ensure_ring(c)) return rc;
-  const size_t len = ring_chunk(n, bytes);
-  const size_t nch = (bytes + len - 1) / len;
-  auto enqueue = [&](size_t ch) -> int {
-    const int sl = int(ch & 1);
-    const size_t off = ch * len, l = std::min(len, bytes - off);
-    ECGPU_HIP(hipMemcpy2DAsync(c->ring[sl], l, d0 + off, dstride, l, n, hipMemcpyDeviceToHost, c->stream));
-    ECGPU_HIP(hipEventRecord(c->ring_ev[sl], c->stream));
-    return ECGPU_OK;
-  };
-  for (size_t ch = 0; ch < std::min<size_t>(2, nch); ++ch)
-    if (int rc = enqueue(ch)) return rc;
-  for (size_t ch = 0; ch < nch; ++ch) {
-    const int sl = int(ch & 1);
-    const size_t off = ch * len, l = std::min(len, bytes - off);
-    ECGPU_HIP(hipEventSynchronize(c->ring_ev[sl]));
-    for (size_t i = 0; i < n; ++i) std::memcpy(hp[i] + off, c->ring[sl] + i * l, l);
-    if (ch + 2 < nch)
-      if (int rc = enqueue(ch + 2)) return rc;
-  }
-  ECGPU_HIP(hipStreamSynchronize(c->stream));
   return ECGPU_OK;
 }
 
@@ -974,7 +885,7 @@ int execute(const FusedOp& op, int64_t size) {
     }
   if (bounce && !staged_hp.empty())
     ECGPU_HIP(hipMemcpyAsync(c->stage, c->bounce, staged_hp.size() * slot, hipMemcpyHostToDevice, c->stream));
-  else if ((rc = stage_in(c, c->stage, slot, staged_hp, size_t(size))) != ECGPU_OK)
+  else if ((rc = copy_shards(true, c->stage, slot, staged_hp, size_t(size), c->stream)) != ECGPU_OK)
     return rc;
 
   std::vector<const uint8_t*> sp(static_cast<size_t>(nsrc));
@@ -1021,16 +932,16 @@ int execute(const FusedOp& op, int64_t size) {
     for (const auto& o : outs) std::memcpy(o.second, c->bounce + (o.first - c->stage), size_t(size));
     return ECGPU_OK;
   }
-  // outputs in consecutive slots: one ring pipeline (or direct DMA); else one by one
+  // outputs in consecutive slots: one 2-D copy per evenly spaced run of host outputs
   bool consecutive = true;
   for (size_t i = 1; i < outs.size() && consecutive; ++i) consecutive = outs[i].first == outs[0].first + i * slot;
   if (consecutive && !outs.empty()) {
     std::vector<char*> hp;
     for (const auto& o : outs) hp.push_back(o.second);
-    if ((rc = stage_out(c, outs[0].first, slot, hp, size_t(size))) != ECGPU_OK) return rc;
+    if ((rc = copy_shards(false, outs[0].first, slot, hp, size_t(size), c->stream)) != ECGPU_OK) return rc;
   } else {
     for (const auto& o : outs)
-      if ((rc = stage_out(c, o.first, slot, {o.second}, size_t(size))) != ECGPU_OK) return rc;
+      ECGPU_HIP(hipMemcpyAsync(o.second, o.first, size_t(size), hipMemcpyDeviceToHost, c->stream));
   }
   ECGPU_HIP(hipStreamSynchronize(c->stream));
   ECGPU_HIP(hipGetLastError());
@@ -1087,7 +998,68 @@ struct ecgpu_accum {
   size_t slot = 0;
   uint8_t* d_acc = nullptr;  // m slots, each `slot` bytes (skewed shard stride)
   std::vector<char> init;
+  // asynchronous adds (ecgpu_accum_add_async): host blocks land in one of two
+  // device block slots on the copy stream while the previous block's fused
+  // update runs on the compute stream
+  uint8_t* d_blk = nullptr;  // 2 block slots
+  hipStream_t s_copy[2] = {nullptr, nullptr}, s_comp = nullptr;  // one copy stream per slot: two DMA queues
+  hipEvent_t loaded[2] = {nullptr, nullptr}, consumed[2] = {nullptr, nullptr};
+  int64_t nasync = 0;  // async adds issued (selects the block slot)
+  bool used[2] = {false, false};
+  bool pending = false;  // async work not yet synchronised
 };
+
+namespace {
+
+// The reference's per-accumulator update (ecx_datanode_main.cpp:699-735) for
+// one arriving block as ONE fused op: coefficient 0 leaves an accumulator
+// alone, 1 copies (first touch) or XORs, any other multiplies (first touch)
+// or multiply-adds.
+FusedOp accum_op(ecgpu_accum* a, const char* block, const int* coefs) {
+  LinearTracker t;
+  char* src = const_cast<char*>(block);
+  for (int i = 0; i < a->m; ++i) {
+    const int c = coefs[i] & 0xFF;
+    if (c == 0) continue;
+    char* acc = ecgpu_accum_device_ptr(a, i);
+    if (c == 1) {
+      if (a->init[i])
+        t.xor3(src, acc, acc);
+      else
+        t.copy(acc, src);
+    } else {
+      t.mul(src, c, acc, a->init[i] != 0);
+    }
+  }
+  return t.finish();
+}
+
+int accum_sync(ecgpu_accum* a) {
+  if (!a->pending) return ECGPU_OK;
+  DeviceGuard g(a->device);
+  for (hipStream_t s : a->s_copy) ECGPU_HIP(hipStreamSynchronize(s));
+  ECGPU_HIP(hipStreamSynchronize(a->s_comp));
+  ECGPU_HIP(hipGetLastError());
+  a->pending = false;
+  return ECGPU_OK;
+}
+
+int accum_async_init(ecgpu_accum* a) {
+  if (a->s_comp) return ECGPU_OK;
+  DeviceGuard g(a->device);
+  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&a->d_blk), 2 * a->slot));
+  // blocking streams: ordered after the caller's null-stream work like every
+  // synchronous call (a device-resident block filled by PyTorch, say)
+  for (hipStream_t& s : a->s_copy) ECGPU_HIP(hipStreamCreateWithFlags(&s, hipStreamDefault));
+  ECGPU_HIP(hipStreamCreateWithFlags(&a->s_comp, hipStreamDefault));
+  for (int i = 0; i < 2; ++i) {
+    ECGPU_HIP(hipEventCreateWithFlags(&a->loaded[i], hipEventDisableTiming));
+    ECGPU_HIP(hipEventCreateWithFlags(&a->consumed[i], hipEventDisableTiming));
+  }
+  return ECGPU_OK;
+}
+
+}  // namespace
 
 ECGPU_API ecgpu_accum* ecgpu_accum_create(int m, int64_t size, int device) {
   if (m <= 0 || size < 0) {
@@ -1117,47 +1089,104 @@ ECGPU_API char* ecgpu_accum_device_ptr(ecgpu_accum* a, int i) {
 
 ECGPU_API int ecgpu_accum_add(ecgpu_accum* a, const char* block, const int* coefs) {
   if (!a || !block || !coefs) return fail(ECGPU_ERR_ARG, "ecgpu_accum_add: bad arguments");
-  LinearTracker t;
-  char* src = const_cast<char*>(block);
-  for (int i = 0; i < a->m; ++i) {  // ecx_datanode_main.cpp:699-735, one accumulator at a time
-    const int c = coefs[i] & 0xFF;
-    if (c == 0) continue;
-    char* acc = ecgpu_accum_device_ptr(a, i);
-    if (c == 1) {
-      if (a->init[i])
-        t.xor3(src, acc, acc);
-      else
-        t.copy(acc, src);
-    } else {
-      t.mul(src, c, acc, a->init[i] != 0);
-    }
-  }
+  if (int rc = accum_sync(a)) return rc;  // after every earlier asynchronous add
   DeviceGuard g(a->device);
-  const int rc = execute(t.finish(), a->size);
+  const int rc = execute(accum_op(a, block, coefs), a->size);
   if (rc != ECGPU_OK) return rc;
   for (int i = 0; i < a->m; ++i)
     if (coefs[i] & 0xFF) a->init[i] = 1;
   return ECGPU_OK;
 }
 
+// Asynchronous add: a host block is copied into a device block slot on the
+// copy stream and the fused update runs on the compute stream, so block j+1
+// crosses PCIe while block j is applied; returns once both are queued.  The
+// block must stay valid and unchanged until ecgpu_accum_sync (or a read, a
+// reset, a synchronous add) returns.
+ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int* coefs) {
+  if (!a || !block || !coefs) return fail(ECGPU_ERR_ARG, "ecgpu_accum_add_async: bad arguments");
+  bool any = false;
+  for (int i = 0; i < a->m; ++i) any |= (coefs[i] & 0xFF) != 0;
+  if (!any || a->size == 0) return ECGPU_OK;
+  if (int rc = accum_async_init(a)) return rc;
+  DeviceGuard g(a->device);
+  bool on_dev = false;
+  if (int rc = classify(block, a->device, &on_dev)) return rc;
+  const char* src = block;
+  int sl = -1;
+  if (!on_dev) {
+    sl = int(a->nasync & 1);
+    // the slot's previous block must have been consumed by its update
+    if (a->used[sl]) ECGPU_HIP(hipStreamWaitEvent(a->s_copy[sl], a->consumed[sl], 0));
+    uint8_t* dst = a->d_blk + size_t(sl) * a->slot;
+    ECGPU_HIP(hipMemcpyAsync(dst, block, size_t(a->size), hipMemcpyHostToDevice, a->s_copy[sl]));
+    ECGPU_HIP(hipEventRecord(a->loaded[sl], a->s_copy[sl]));
+    ECGPU_HIP(hipStreamWaitEvent(a->s_comp, a->loaded[sl], 0));
+    src = reinterpret_cast<const char*>(dst);
+    ++a->nasync;
+  }
+  a->pending = true;
+  const FusedOp op = accum_op(a, src, coefs);
+  add_stats(op);
+  if (inline_ok(op)) {
+    std::vector<const uint8_t*> sp;
+    for (void* p : op.srcs) sp.push_back(static_cast<const uint8_t*>(p));
+    std::vector<uint8_t*> dp;
+    for (void* p : op.dsts) dp.push_back(static_cast<uint8_t*>(p));
+    if (int rc = launch_inline(op, sp, dp, a->size, a->s_comp)) return rc;
+  } else {
+    // engine override or > 4 aliased rows: the synchronous path
+    if (int rc = accum_sync(a)) return rc;
+    if (int rc = execute(op, a->size)) return rc;
+  }
+  if (sl >= 0) {
+    ECGPU_HIP(hipEventRecord(a->consumed[sl], a->s_comp));
+    a->used[sl] = true;
+  }
+  for (int i = 0; i < a->m; ++i)
+    if (coefs[i] & 0xFF) a->init[i] = 1;
+  return ECGPU_OK;
+}
+
+ECGPU_API int ecgpu_accum_sync(ecgpu_accum* a) {
+  if (!a) return fail(ECGPU_ERR_ARG, "ecgpu_accum_sync: null");
+  return accum_sync(a);
+}
+
 ECGPU_API int ecgpu_accum_read(ecgpu_accum* a, int i, char* out, int64_t nbytes) {
   if (!a || i < 0 || i >= a->m || !out || nbytes < 0 || nbytes > a->size)
     return fail(ECGPU_ERR_ARG, "ecgpu_accum_read: bad arguments");
+  if (int rc = accum_sync(a)) return rc;
   if (!a->init[i]) return ECGPU_ERR;
   DeviceGuard g(a->device);
-  ECGPU_HIP(hipMemcpy(out, ecgpu_accum_device_ptr(a, i), size_t(nbytes), hipMemcpyDefault));
+  if (a->s_comp) {  // on the accumulator's own stream, not the device-wide null stream
+    ECGPU_HIP(hipMemcpyAsync(out, ecgpu_accum_device_ptr(a, i), size_t(nbytes), hipMemcpyDefault, a->s_comp));
+    ECGPU_HIP(hipStreamSynchronize(a->s_comp));
+  } else {
+    ECGPU_HIP(hipMemcpy(out, ecgpu_accum_device_ptr(a, i), size_t(nbytes), hipMemcpyDefault));
+  }
   return ECGPU_OK;
 }
 
 ECGPU_API int ecgpu_accum_reset(ecgpu_accum* a) {
   if (!a) return fail(ECGPU_ERR_ARG, "ecgpu_accum_reset: null");
+  if (int rc = accum_sync(a)) return rc;
   std::fill(a->init.begin(), a->init.end(), 0);
   return ECGPU_OK;
 }
 
 ECGPU_API void ecgpu_accum_destroy(ecgpu_accum* a) {
   if (!a) return;
+  (void)accum_sync(a);
   DeviceGuard g(a->device);
+  for (int i = 0; i < 2; ++i) {
+    if (a->loaded[i]) (void)hipEventDestroy(a->loaded[i]);
+    if (a->consumed[i]) (void)hipEventDestroy(a->consumed[i]);
+  }
+  for (hipStream_t s : a->s_copy)
+    if (s) (void)hipStreamDestroy(s);
+  if (a->s_comp) (void)hipStreamDestroy(a->s_comp);
+  if (a->d_blk) (void)hipFree(a->d_blk);
   if (a->d_acc) (void)hipFree(a->d_acc);
   delete a;
 }
@@ -1287,18 +1316,15 @@ ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create_decode(int k, int m, int w, cons
 }
 
 
-ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, char** coding_ptrs) {
-  if (!p || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_submit: bad arguments");
-  std::lock_guard<std::mutex> lk(p->mu);
-  DeviceGuard g(p->device);
+namespace {
+// Queues stripe t into ring slot t % depth: H2D of the sources (s_h2d), the
+// fused apply (s_comp), D2H of the outputs (s_d2h).
+int pipeline_enqueue(ecgpu_pipeline* p, int sl, char** data_ptrs, char** coding_ptrs) {
   auto host = [&](int id) { return id < p->k ? data_ptrs[id] : coding_ptrs[id - p->k]; };
-  const int64_t t = p->next_ticket;
-  const int sl = int(t % p->depth);
-  int rc = pipeline_retire(p, sl);  // the slot's previous stripe must be out
-  if (rc != ECGPU_OK) return rc;
   const int ns = p->nsrc(), nr = p->rows();
   const size_t bytes = size_t(p->size);
   std::vector<char*> hp;
+  int rc = ECGPU_OK;
   if (nr > 0) {  // nothing to read when no shard is written
     for (int j = 0; j < ns; ++j) hp.push_back(host(p->src_ids[j]));
     if ((rc = copy_shards(true, p->slot_shard(sl, 0), p->slot_stride, hp, bytes, p->s_h2d)) != ECGPU_OK) return rc;
@@ -1306,8 +1332,7 @@ ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, cha
   ECGPU_HIP(hipEventRecord(p->loaded[sl], p->s_h2d));
   ECGPU_HIP(hipStreamWaitEvent(p->s_comp, p->loaded[sl], 0));
   if (ns > 0 && nr > 0) {
-    rc = plan_launch(p->plans[sl], p->s_comp);
-    if (rc != ECGPU_OK) return rc;
+    if ((rc = plan_launch(p->plans[sl], p->s_comp)) != ECGPU_OK) return rc;
   } else {
     for (int i = 0; i < nr; ++i)  // rows with no source: all-zero output
       ECGPU_HIP(hipMemsetAsync(p->slot_shard(sl, ns + i), 0, bytes, p->s_comp));
@@ -1318,6 +1343,27 @@ ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, cha
   for (int i = 0; i < nr; ++i) hp.push_back(host(p->out_ids[i]));
   if ((rc = copy_shards(false, p->slot_shard(sl, ns), p->slot_stride, hp, bytes, p->s_d2h)) != ECGPU_OK) return rc;
   ECGPU_HIP(hipEventRecord(p->drained[sl], p->s_d2h));
+  return ECGPU_OK;
+}
+}  // namespace
+
+ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, char** coding_ptrs) {
+  if (!p || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_submit: bad arguments");
+  std::lock_guard<std::mutex> lk(p->mu);
+  DeviceGuard g(p->device);
+  const int64_t t = p->next_ticket;
+  const int sl = int(t % p->depth);
+  int rc = pipeline_retire(p, sl);  // the slot's previous stripe must be out
+  if (rc != ECGPU_OK) return rc;
+  rc = pipeline_enqueue(p, sl, data_ptrs, coding_ptrs);
+  if (rc != ECGPU_OK) {
+    // part of the stripe may already be queued against the caller's buffers:
+    // let it finish before reporting, so no DMA outlives the failed call
+    const std::string msg = t_err;
+    for (hipStream_t s : {p->s_h2d, p->s_comp, p->s_d2h}) (void)hipStreamSynchronize(s);
+    t_err = msg;
+    return rc;
+  }
   p->slot_ticket[sl] = t;
   p->next_ticket = t + 1;
   return t;
@@ -1328,7 +1374,7 @@ ECGPU_API int ecgpu_pipeline_wait(ecgpu_pipeline* p, int64_t ticket) {
   std::lock_guard<std::mutex> lk(p->mu);
   if (ticket < p->done_below) return ECGPU_OK;
   if (ticket >= p->next_ticket) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_wait: ticket not submitted");
-  DeviceGuard g(p->device);
+  // (event waits need no current-device switch)
   // retire every slot up to and including the ticket's (completion is in order)
   for (int64_t t = p->done_below; t <= ticket; ++t) {
     const int rc = pipeline_retire(p, int(t % p->depth));
@@ -1352,24 +1398,85 @@ ECGPU_API void ecgpu_pipeline_destroy(ecgpu_pipeline* p) {
 // ---------------------------------------------- multi-device pipeline ----
 // Stripes are independent, so a process driving several GPUs
 // shards them round-robin: stripe t runs on member t % n as that member's
-// local ticket t / n.  No collective and no cross-device traffic; each member
-// is a complete single-device pipeline with its own ring and streams, and
-// the submit path only enqueues asynchronous work, so one host thread keeps
-// every device busy.
-struct ecgpu_pipeline_group {
-  std::vector<ecgpu_pipeline*> members;
-  int64_t next_ticket = 0;
+// local ticket t / n.  No collective and no cross-device traffic.  Each
+// member is a complete single-device pipeline with its own ring and streams
+// AND its own submit thread, bound to its device once (hipSetDevice at
+// thread start, never again): group_submit only hands the stripe's pointer
+// lists to member t % n's queue (a per-member lock; tickets come from an
+// atomic counter, no group-wide lock) and returns, the worker issues the
+// stripe's copies and launch, so pageable staging on one device never holds
+// up another.  Waits sync on the member's events (no device switch).
+namespace {
+struct GroupJob {
+  std::vector<char*> data, coding;
+};
+
+struct GroupMember {
+  ecgpu_pipeline* p = nullptr;
+  int k = 0, m = 0, cap = 1;
+  std::thread worker;
   std::mutex mu;
+  std::condition_variable cv_job, cv_done, cv_space;
+  std::map<int64_t, GroupJob> pending;  // local ticket -> job, handed in possibly out of order
+  int64_t next_local = 0;               // next local ticket the worker submits
+  int64_t failed_from = -1;             // first local ticket whose submit failed (sticky)
+  int failed_rc = ECGPU_OK;
+  std::string failed_msg;
+  bool stop = false;
+
+  void run() {
+    (void)hipSetDevice(p->device);  // once: every submit below runs on this device
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv_job.wait(lk, [&] { return stop || pending.count(next_local) != 0; });
+      auto it = pending.find(next_local);
+      if (it == pending.end()) return;  // stop, queue drained
+      GroupJob job = std::move(it->second);
+      pending.erase(it);
+      cv_space.notify_all();
+      int64_t r = 0;
+      if (failed_from < 0) {
+        lk.unlock();
+        r = ecgpu_pipeline_submit(p, job.data.data(), job.coding.data());
+        const std::string msg = r < 0 ? t_err : std::string();
+        lk.lock();
+        if (r < 0) {
+          failed_from = next_local;
+          failed_rc = int(r);
+          failed_msg = msg;
+        }
+      }
+      ++next_local;
+      cv_done.notify_all();
+    }
+  }
+};
+}  // namespace
+
+struct ecgpu_pipeline_group {
+  std::vector<std::unique_ptr<GroupMember>> members;
+  std::atomic<int64_t> next_ticket{0};
 };
 
 namespace {
 void group_free(ecgpu_pipeline_group* g) {
   if (!g) return;
-  for (auto* p : g->members) ecgpu_pipeline_destroy(p);
+  for (auto& mb : g->members) {
+    if (mb->worker.joinable()) {
+      {
+        std::lock_guard<std::mutex> lk(mb->mu);
+        mb->stop = true;
+      }
+      mb->cv_job.notify_all();
+      mb->worker.join();
+    }
+    ecgpu_pipeline_destroy(mb->p);
+  }
   delete g;
 }
 
-ecgpu_pipeline_group* group_build(int ndev, const int* devices, const std::function<ecgpu_pipeline*(int)>& make) {
+ecgpu_pipeline_group* group_build(int ndev, const int* devices, int k, int m, int depth,
+                                  const std::function<ecgpu_pipeline*(int)>& make) {
   if (ndev <= 0 || !devices) {
     fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group: ndev > 0 and a device list required");
     return nullptr;
@@ -1378,10 +1485,21 @@ ecgpu_pipeline_group* group_build(int ndev, const int* devices, const std::funct
   for (int i = 0; i < ndev; ++i) {
     ecgpu_pipeline* p = make(devices[i]);
     if (!p) {  // make() left the message in ecgpu_last_error
+      const std::string msg = t_err;
       group_free(g);
+      t_err = msg;
       return nullptr;
     }
-    g->members.push_back(p);
+    auto mb = std::make_unique<GroupMember>();
+    mb->p = p;
+    mb->k = k;
+    mb->m = m;
+    mb->cap = std::max(1, depth);
+    g->members.push_back(std::move(mb));
+  }
+  for (auto& mb : g->members) {
+    GroupMember* raw = mb.get();
+    raw->worker = std::thread([raw] { raw->run(); });
   }
   return g;
 }
@@ -1389,54 +1507,68 @@ ecgpu_pipeline_group* group_build(int ndev, const int* devices, const std::funct
 
 ECGPU_API ecgpu_pipeline_group* ecgpu_pipeline_group_create(int k, int m, const int* matrix, int64_t size, int depth,
                                                             int ndev, const int* devices) {
-  return group_build(ndev, devices,
+  return group_build(ndev, devices, k, m, depth,
                      [&](int dev) { return ecgpu_pipeline_create(k, m, matrix, size, depth, dev); });
 }
 
 ECGPU_API ecgpu_pipeline_group* ecgpu_pipeline_group_create_decode(int k, int m, int w, const int* matrix,
                                                                    int row_k_ones, const int* erasures, int64_t size,
                                                                    int depth, int ndev, const int* devices) {
-  return group_build(ndev, devices, [&](int dev) {
+  return group_build(ndev, devices, k, m, depth, [&](int dev) {
     return ecgpu_pipeline_create_decode(k, m, w, matrix, row_k_ones, erasures, size, depth, dev);
   });
 }
 
 ECGPU_API int64_t ecgpu_pipeline_group_submit(ecgpu_pipeline_group* g, char** data_ptrs, char** coding_ptrs) {
   if (!g || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_submit: bad arguments");
-  std::lock_guard<std::mutex> lk(g->mu);
-  const int64_t t = g->next_ticket;
   const int64_t n = int64_t(g->members.size());
-  const int64_t local = ecgpu_pipeline_submit(g->members[size_t(t % n)], data_ptrs, coding_ptrs);
-  if (local < 0) return local;
-  if (local != t / n) return fail(ECGPU_ERR, "ecgpu_pipeline_group_submit: member ticket out of sequence");
-  g->next_ticket = t + 1;
+  const int64_t t = g->next_ticket.fetch_add(1);
+  GroupMember& mb = *g->members[size_t(t % n)];
+  GroupJob job;
+  job.data.assign(data_ptrs, data_ptrs + mb.k);
+  job.coding.assign(coding_ptrs, coding_ptrs + mb.m);
+  {
+    std::unique_lock<std::mutex> lk(mb.mu);
+    // back-pressure: at most `depth` stripes queued ahead of the worker
+    mb.cv_space.wait(lk, [&] { return int64_t(mb.pending.size()) < mb.cap || t / n <= mb.next_local; });
+    mb.pending.emplace(t / n, std::move(job));
+  }
+  mb.cv_job.notify_one();
   return t;
 }
 
 ECGPU_API int ecgpu_pipeline_group_wait(ecgpu_pipeline_group* g, int64_t ticket) {
   if (!g || ticket < 0) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_wait: bad arguments");
-  int64_t next, n;
+  if (ticket >= g->next_ticket.load()) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_wait: ticket not submitted");
+  const int64_t n = int64_t(g->members.size());
+  GroupMember& mb = *g->members[size_t(ticket % n)];
+  const int64_t local = ticket / n;
   {
-    std::lock_guard<std::mutex> lk(g->mu);
-    next = g->next_ticket;
-    n = int64_t(g->members.size());
+    std::unique_lock<std::mutex> lk(mb.mu);
+    mb.cv_done.wait(lk, [&] { return mb.next_local > local; });  // the worker has queued it
+    if (mb.failed_from >= 0 && local >= mb.failed_from) return fail(mb.failed_rc, mb.failed_msg);
   }
-  if (ticket >= next) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_wait: ticket not submitted");
-  return ecgpu_pipeline_wait(g->members[size_t(ticket % n)], ticket / n);
+  return ecgpu_pipeline_wait(mb.p, local);
 }
 
 ECGPU_API int ecgpu_pipeline_group_drain(ecgpu_pipeline_group* g) {
   if (!g) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_drain: null");
-  for (auto* p : g->members) {
-    const int rc = ecgpu_pipeline_drain(p);
-    if (rc != ECGPU_OK) return rc;
+  const int64_t end = g->next_ticket.load(), n = int64_t(g->members.size());
+  int rc = ECGPU_OK;
+  for (int64_t t = std::max<int64_t>(0, end - n); t < end; ++t) {  // each member's last ticket
+    const int r = ecgpu_pipeline_group_wait(g, t);
+    if (r != ECGPU_OK && rc == ECGPU_OK) rc = r;
   }
-  return ECGPU_OK;
+  return rc;
 }
 
 ECGPU_API int ecgpu_pipeline_group_size(ecgpu_pipeline_group* g) { return g ? int(g->members.size()) : 0; }
 
-ECGPU_API void ecgpu_pipeline_group_destroy(ecgpu_pipeline_group* g) { group_free(g); }
+ECGPU_API void ecgpu_pipeline_group_destroy(ecgpu_pipeline_group* g) {
+  if (!g) return;
+  (void)ecgpu_pipeline_group_drain(g);
+  group_free(g);
+}
 
 ECGPU_API int ecgpu_host_register(void* ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return fail(ECGPU_ERR_ARG, "ecgpu_host_register: bad arguments");

@@ -80,8 +80,10 @@ class HostPipeline:
 class HostPipelineGroup:
     """Several GPUs from one process (ecgpu_pipeline_group_*): one
     single-device pipeline per entry of ``devices`` (repeats allowed), stripe
-    ticket t on member t % len(devices).  Stripes are independent, so there is
-    no collective; the interface is HostPipeline's."""
+    ticket t on member t % len(devices), each member with its own submit
+    thread bound to its device.  Stripes are independent, so there is no
+    collective; the interface is HostPipeline's (submit may be called from
+    several threads)."""
 
     def __init__(self, k: int, m: int, matrix: Sequence[int], size: int, devices: Sequence[int], depth: int = 3,
                  _handle=None):
@@ -121,7 +123,11 @@ class HostPipelineGroup:
 
     def wait(self, ticket: int) -> None:
         N.check(N.lib.ecgpu_pipeline_group_wait(self._g, ticket), "ecgpu_pipeline_group_wait")
-        self._keep.pop(ticket, None)
+        # a member completes its tickets in order: every earlier ticket of the
+        # same member is done too, so its buffers are released as well
+        n = len(self.devices)
+        for t in [t for t in self._keep if t <= ticket and t % n == ticket % n]:
+            del self._keep[t]
 
     def drain(self) -> None:
         N.check(N.lib.ecgpu_pipeline_group_drain(self._g), "ecgpu_pipeline_group_drain")

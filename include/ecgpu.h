@@ -172,10 +172,17 @@ ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p);
  * first-touch semantics: coefficient 0 leaves an accumulator untouched, 1
  * copies (first touch) or XORs, anything else multiplies (first touch) or
  * multiply-XORs.  Only the block crosses PCIe per arrival; parity is read
- * out once with ecgpu_accum_read.  All calls are synchronous. */
+ * out once with ecgpu_accum_read.  ecgpu_accum_add is synchronous;
+ * ecgpu_accum_add_async only queues the block's copy (copy stream, two
+ * device block slots) and its update (compute stream), so the next block's
+ * H2D overlaps this block's update -- its block must stay valid and unchanged
+ * until ecgpu_accum_sync, a read, a reset or a synchronous add returns (each
+ * of which waits for every queued add). */
 typedef struct ecgpu_accum ecgpu_accum;
 ECGPU_API ecgpu_accum* ecgpu_accum_create(int m, int64_t size, int device);
 ECGPU_API int ecgpu_accum_add(ecgpu_accum* a, const char* block, const int* coefs /* m */);
+ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int* coefs /* m */);
+ECGPU_API int ecgpu_accum_sync(ecgpu_accum* a);
 ECGPU_API int ecgpu_accum_read(ecgpu_accum* a, int i, char* out, int64_t nbytes); /* -1 if never touched */
 ECGPU_API char* ecgpu_accum_device_ptr(ecgpu_accum* a, int i);
 ECGPU_API int ecgpu_accum_reset(ecgpu_accum* a);

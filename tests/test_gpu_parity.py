@@ -406,6 +406,35 @@ def test_ecx_parity_accumulator(ec, gpu, restatement, k, m, bs, where):
     acc.close()
 
 
+@pytest.mark.parametrize("where", ["host", "pinned", "device"])
+@pytest.mark.parametrize("k,m,bs", [(10, 4, (1 << 20) + 5), (5, 6, 4099), (3, 3, (1 << 20) // 3)])
+def test_ecx_parity_accumulator_async(ec, gpu, restatement, where, k, m, bs):
+    # queued adds (copy of block j+1 overlapping the update of block j), one
+    # synchronous add in the middle, two stripes through the same
+    # accumulators; m = 6 > 4 aliased rows takes the synchronous fallback
+    import torch
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    acc = ec.ParityAccumulator(m, bs)
+    for stripe in range(2):
+        blocks = host_shards(39, stripe, k, bs)
+        for j in range(k):
+            if where == "device":
+                blk = to_dev([blocks[j]], gpu)[0]
+            elif where == "pinned":
+                blk = torch.from_numpy(np.ascontiguousarray(blocks[j])).pin_memory()
+            else:
+                blk = blocks[j]
+            acc.add(blk, [M[i * k + j] for i in range(m)], wait=(j == k // 2))
+        acc.sync()
+        ref = _encode_ref(restatement, k, m, M, blocks, bs)
+        for i in range(m):
+            out = np.zeros(bs, np.uint8)
+            assert acc.read(i, out)
+            assert np.array_equal(out, ref[i][:bs]), (stripe, i)
+        acc.reset()
+    acc.close()
+
+
 def test_ecx_accumulator_zero_coefficients_and_reset(ec, gpu, restatement):
     k, m, bs = 4, 3, 4099
     coef = [[0, 0, 0, 0], [1, 0, 7, 1], [0, 29, 1, 142]]  # row 0 never touched
@@ -622,6 +651,49 @@ def test_pipeline_group_encode_round_robin(ec, gpu, restatement, members):
         for i in range(m):
             assert np.array_equal(coding[s][i].numpy()[:size], ref[i][:size]), (s, i)
             assert not coding[s][i].numpy()[size:].any()
+
+
+def test_pipeline_group_concurrent_submitters(ec, gpu, restatement):
+    # per-member submit workers, no group-wide lock: four host threads submit
+    # interleaved stripes (pageable and pinned) into one group of three
+    # members and wait on their own tickets out of order
+    import threading
+
+    import torch
+    k, m, size, per_thread, nthreads = 6, 3, (1 << 17) + 3, 5, 4
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    g = ec.HostPipelineGroup(k, m, M, size, devices=[0, 0, 0], depth=2)
+    results, errors = {}, []
+
+    def run(tid):
+        try:
+            mine = []
+            for i in range(per_thread):
+                s = tid * per_thread + i
+                d = host_shards(62, s, k, size)
+                c = alloc_shards(m, size, PAD)
+                if s % 2:
+                    d = [torch.from_numpy(b).pin_memory() for b in d]
+                    c = [torch.from_numpy(b).pin_memory() for b in c]
+                mine.append((s, g.submit(d, c), d, c))
+            for s, t, d, c in reversed(mine):
+                g.wait(t)
+                results[s] = ([np.asarray(b)[:size].copy() for b in d], [np.asarray(b)[:size].copy() for b in c])
+        except Exception as ex:  # reported below
+            errors.append(repr(ex))
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(nthreads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    g.close()
+    assert not errors, errors
+    assert sorted(results) == list(range(per_thread * nthreads))
+    for s, (d, c) in results.items():
+        ref = _encode_ref(restatement, k, m, M, d, size)
+        for i in range(m):
+            assert np.array_equal(c[i], ref[i][:size]), (s, i)
 
 
 def test_pipeline_group_decoder(ec, gpu):

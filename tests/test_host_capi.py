@@ -169,3 +169,10 @@ def test_hot_path_without_gpu_fails_loudly():
             "f(a.ctypes.data, a.ctypes.data, a.ctypes.data, 64)\n")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "MI355X path failed" in r.stderr
+
+
+def test_int_array_accepts_any_iterable():
+    from erasure_coding_test_amd import _native as N
+    assert list(N.int_array(x for x in range(3))) == [0, 1, 2]
+    assert list(N.int_array(iter(range(100)))) == list(range(100))  # the numpy branch
+    assert list(N.int_array([2**32 - 1])) == [-1]  # wraps like a C int

@@ -232,41 +232,56 @@ def ecx_accum(k=10, m=4, S=4 << 20, stripes=12):
     accumulators, then m reads of the finished parity.  Blocks device-resident,
     in pinned host memory, or in pageable host memory; the parity read goes to
     the same kind of memory.  HBM bytes per stripe: k blocks read, m
-    accumulators written once and read+written k-1 times."""
+    accumulators written once and read+written k-1 times.  *_async: the adds
+    are queued (ecgpu_accum_add_async: block j+1's H2D overlaps block j's
+    update) and sync() waits for them.  per_add_us = (k adds + sync) / k;
+    per_read_us = one parity read-out; stripe_ms = both."""
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     cols = [[M[i * k + j] for i in range(m)] for j in range(k)]
     out = {}
-    for where in ("device", "pinned", "pageable"):
-        if where == "device":
+    for where in ("device", "pinned", "pageable", "device_async", "pinned_async", "pageable_async"):
+        wait = not where.endswith("_async")
+        if where.startswith("device"):
             blocks = torch.randint(0, 256, (k, S), dtype=torch.uint8, device="cuda")
             parity = torch.empty((m, S), dtype=torch.uint8, device="cuda")
         else:
             blocks = torch.randint(0, 256, (k, S), dtype=torch.uint8)
             parity = torch.empty((m, S), dtype=torch.uint8)
-            if where == "pinned":
+            if where.startswith("pinned"):
                 blocks, parity = blocks.pin_memory(), parity.pin_memory()
         acc = E.ParityAccumulator(m, S)
 
-        def one():
+        def adds():
             acc.reset()
             for j in range(k):
-                acc.add(blocks[j], cols[j])
+                acc.add(blocks[j], cols[j], wait=wait)
+            acc.sync()
+
+        def reads():
             for i in range(m):
                 acc.read(i, parity[i])
 
-        one()
+        adds()
+        reads()
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
+        ta = tr = 0.0
         for _ in range(stripes):
-            one()
+            t0 = time.perf_counter()
+            adds()
+            t1 = time.perf_counter()
+            reads()
+            ta += t1 - t0
+            tr += time.perf_counter() - t1
         torch.cuda.synchronize()
-        t = (time.perf_counter() - t0) / stripes
+        t = (ta + tr) / stripes
         hbm = (k + m + 2 * m * (k - 1)) * S
-        out[where] = {"stripe_ms": round(t * 1e3, 3), "per_add_us": round(t / k * 1e6, 1),
+        out[where] = {"stripe_ms": round(t * 1e3, 3), "per_add_us": round(ta / stripes / k * 1e6, 1),
+                      "per_read_us": round(tr / stripes / m * 1e6, 1),
+                      "add_GiBps": round(k * S * stripes / ta / GiB, 2),
                       "data_GiBps": round(k * S / t / GiB, 2), "hbm_GBps_if_device": round(hbm / t / 1e9, 1)}
         acc.close()
     return {"workload": f"ParityAccumulator RS({k},{m}), {S >> 20} MiB blocks, {k} adds + {m} reads per stripe, "
-                        f"{stripes} stripes, synchronous calls", "results": out}
+                        f"{stripes} stripes, synchronous or queued adds", "results": out}
 
 
 def call_latency(reps=200):

@@ -459,6 +459,7 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
     int mul_terms = 0;  // coefficients that are neither 0 nor 1
     for (int r = 0; r < R; ++r)
       for (int j = 0; j < K; ++j) mul_terms += p->coef[size_t(r0 + r) * K + j] > 1u;
+    // (the LDS engine runs uncapped: capping it cost 4 % encode, 16 % decode{0})
     const bool cap = p->kind == ECGPU_KERNEL_PERM && cap_for(K, R, mul_terms);
     uint64_t unit = 0, zero = 0;
     if (spec)
@@ -998,15 +999,13 @@ struct ecgpu_accum {
   size_t slot = 0;
   uint8_t* d_acc = nullptr;  // m slots, each `slot` bytes (skewed shard stride)
   std::vector<char> init;
-  // asynchronous adds (ecgpu_accum_add_async): host blocks land in one of two
-  // device block slots on the copy stream while the previous block's fused
-  // update runs on the compute stream
-  uint8_t* d_blk = nullptr;  // 2 block slots
-  hipStream_t s_copy[2] = {nullptr, nullptr}, s_comp = nullptr;  // one copy stream per slot: two DMA queues
-  hipEvent_t loaded[2] = {nullptr, nullptr}, consumed[2] = {nullptr, nullptr};
-  int64_t nasync = 0;  // async adds issued (selects the block slot)
-  bool used[2] = {false, false};
-  bool pending = false;  // async work not yet synchronised
+  // queued adds (ecgpu_accum_add_async): a host block is copied into the
+  // device block buffer and applied, both on the accumulator's own stream,
+  // and the call returns; the copy of block j+1 queues behind the update of
+  // block j (stream order protects the buffer) with no host round trip
+  uint8_t* d_blk = nullptr;
+  hipStream_t stream = nullptr;
+  bool pending = false;  // queued work not yet synchronised
 };
 
 namespace {
@@ -1036,26 +1035,19 @@ FusedOp accum_op(ecgpu_accum* a, const char* block, const int* coefs) {
 
 int accum_sync(ecgpu_accum* a) {
   if (!a->pending) return ECGPU_OK;
-  DeviceGuard g(a->device);
-  for (hipStream_t s : a->s_copy) ECGPU_HIP(hipStreamSynchronize(s));
-  ECGPU_HIP(hipStreamSynchronize(a->s_comp));
+  ECGPU_HIP(hipStreamSynchronize(a->stream));
   ECGPU_HIP(hipGetLastError());
   a->pending = false;
   return ECGPU_OK;
 }
 
 int accum_async_init(ecgpu_accum* a) {
-  if (a->s_comp) return ECGPU_OK;
+  if (a->stream) return ECGPU_OK;
   DeviceGuard g(a->device);
-  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&a->d_blk), 2 * a->slot));
-  // blocking streams: ordered after the caller's null-stream work like every
+  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&a->d_blk), a->slot));
+  // a blocking stream: ordered after the caller's null-stream work like every
   // synchronous call (a device-resident block filled by PyTorch, say)
-  for (hipStream_t& s : a->s_copy) ECGPU_HIP(hipStreamCreateWithFlags(&s, hipStreamDefault));
-  ECGPU_HIP(hipStreamCreateWithFlags(&a->s_comp, hipStreamDefault));
-  for (int i = 0; i < 2; ++i) {
-    ECGPU_HIP(hipEventCreateWithFlags(&a->loaded[i], hipEventDisableTiming));
-    ECGPU_HIP(hipEventCreateWithFlags(&a->consumed[i], hipEventDisableTiming));
-  }
+  ECGPU_HIP(hipStreamCreateWithFlags(&a->stream, hipStreamDefault));
   return ECGPU_OK;
 }
 
@@ -1098,11 +1090,14 @@ ECGPU_API int ecgpu_accum_add(ecgpu_accum* a, const char* block, const int* coef
   return ECGPU_OK;
 }
 
-// Asynchronous add: a host block is copied into a device block slot on the
-// copy stream and the fused update runs on the compute stream, so block j+1
-// crosses PCIe while block j is applied; returns once both are queued.  The
-// block must stay valid and unchanged until ecgpu_accum_sync (or a read, a
-// reset, a synchronous add) returns.
+// Queued add: the block's H2D copy (host blocks, into the device block
+// buffer) and its fused update go onto the accumulator's stream and the
+// call returns, so consecutive blocks stream over PCIe back to back with no
+// host round trip per block.  (A second copy stream overlapping block j+1's
+// H2D with block j's ~6 us update measured slower: the cross-stream event
+// waits cost more than the overlap buys)  The block must stay
+// valid and unchanged until ecgpu_accum_sync (or a read, a reset, a
+// synchronous add) returns.
 ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int* coefs) {
   if (!a || !block || !coefs) return fail(ECGPU_ERR_ARG, "ecgpu_accum_add_async: bad arguments");
   bool any = false;
@@ -1113,35 +1108,23 @@ ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int
   bool on_dev = false;
   if (int rc = classify(block, a->device, &on_dev)) return rc;
   const char* src = block;
-  int sl = -1;
   if (!on_dev) {
-    sl = int(a->nasync & 1);
-    // the slot's previous block must have been consumed by its update
-    if (a->used[sl]) ECGPU_HIP(hipStreamWaitEvent(a->s_copy[sl], a->consumed[sl], 0));
-    uint8_t* dst = a->d_blk + size_t(sl) * a->slot;
-    ECGPU_HIP(hipMemcpyAsync(dst, block, size_t(a->size), hipMemcpyHostToDevice, a->s_copy[sl]));
-    ECGPU_HIP(hipEventRecord(a->loaded[sl], a->s_copy[sl]));
-    ECGPU_HIP(hipStreamWaitEvent(a->s_comp, a->loaded[sl], 0));
-    src = reinterpret_cast<const char*>(dst);
-    ++a->nasync;
+    ECGPU_HIP(hipMemcpyAsync(a->d_blk, block, size_t(a->size), hipMemcpyHostToDevice, a->stream));
+    src = reinterpret_cast<const char*>(a->d_blk);
   }
   a->pending = true;
   const FusedOp op = accum_op(a, src, coefs);
-  add_stats(op);
   if (inline_ok(op)) {
+    add_stats(op);
     std::vector<const uint8_t*> sp;
     for (void* p : op.srcs) sp.push_back(static_cast<const uint8_t*>(p));
     std::vector<uint8_t*> dp;
     for (void* p : op.dsts) dp.push_back(static_cast<uint8_t*>(p));
-    if (int rc = launch_inline(op, sp, dp, a->size, a->s_comp)) return rc;
+    if (int rc = launch_inline(op, sp, dp, a->size, a->stream)) return rc;
   } else {
     // engine override or > 4 aliased rows: the synchronous path
     if (int rc = accum_sync(a)) return rc;
     if (int rc = execute(op, a->size)) return rc;
-  }
-  if (sl >= 0) {
-    ECGPU_HIP(hipEventRecord(a->consumed[sl], a->s_comp));
-    a->used[sl] = true;
   }
   for (int i = 0; i < a->m; ++i)
     if (coefs[i] & 0xFF) a->init[i] = 1;
@@ -1159,9 +1142,9 @@ ECGPU_API int ecgpu_accum_read(ecgpu_accum* a, int i, char* out, int64_t nbytes)
   if (int rc = accum_sync(a)) return rc;
   if (!a->init[i]) return ECGPU_ERR;
   DeviceGuard g(a->device);
-  if (a->s_comp) {  // on the accumulator's own stream, not the device-wide null stream
-    ECGPU_HIP(hipMemcpyAsync(out, ecgpu_accum_device_ptr(a, i), size_t(nbytes), hipMemcpyDefault, a->s_comp));
-    ECGPU_HIP(hipStreamSynchronize(a->s_comp));
+  if (a->stream) {  // on the accumulator's own stream, not the device-wide null stream
+    ECGPU_HIP(hipMemcpyAsync(out, ecgpu_accum_device_ptr(a, i), size_t(nbytes), hipMemcpyDefault, a->stream));
+    ECGPU_HIP(hipStreamSynchronize(a->stream));
   } else {
     ECGPU_HIP(hipMemcpy(out, ecgpu_accum_device_ptr(a, i), size_t(nbytes), hipMemcpyDefault));
   }
@@ -1179,13 +1162,7 @@ ECGPU_API void ecgpu_accum_destroy(ecgpu_accum* a) {
   if (!a) return;
   (void)accum_sync(a);
   DeviceGuard g(a->device);
-  for (int i = 0; i < 2; ++i) {
-    if (a->loaded[i]) (void)hipEventDestroy(a->loaded[i]);
-    if (a->consumed[i]) (void)hipEventDestroy(a->consumed[i]);
-  }
-  for (hipStream_t s : a->s_copy)
-    if (s) (void)hipStreamDestroy(s);
-  if (a->s_comp) (void)hipStreamDestroy(a->s_comp);
+  if (a->stream) (void)hipStreamDestroy(a->stream);
   if (a->d_blk) (void)hipFree(a->d_blk);
   if (a->d_acc) (void)hipFree(a->d_acc);
   delete a;

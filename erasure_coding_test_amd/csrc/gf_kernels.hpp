@@ -18,10 +18,10 @@
 //    compile-time structure the host checks per launch.  K and R are
 //    compile-time; gf_apply_perm_generic covers K > 16 and gf_apply_bytes
 //    shard tails and misaligned pointers.
-//  * gf_apply_lds<K,R> (w = 8, selectable): per coefficient the two
-//    16-entry nibble tables T_lo[x] = c*x, T_hi[x] = c*(x<<4) live in LDS and
-//    every byte costs 2 ds_read_u8 (LDS-issue-bound; also the bench's
-//    independent self-check engine).
+//  * gf_apply_lds<K,R> (w = 8, selectable; the bench's independent
+//    self-check engine): the north star's nibble tables T_lo[x] = c*x,
+//    T_hi[x] = c*(x<<4) staged in LDS, one 4-byte entry serving all R rows
+//    of a nibble (2 ds_read_b32 per source byte for every row together).
 //  * gf_apply_wide_nib<R> / gf_apply_wide<W,R> (w = 16 / 32) and
 //    gf_xor_packets16 / gf_xor_packets (GF(2) bit-matrix / schedule coding):
 //    see their sections below.
@@ -636,22 +636,40 @@ __global__ __launch_bounds__(kBlock) void diag_copy(ApplyArgs a) {
 }
 
 // ----------------------------------------------------------------- LDS ----
-__device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t* t, uint32_t lo, uint32_t hi) {
-  // lo/hi hold the low/high nibble of each byte in byte lanes 0..3.
-  uint32_t p = 0;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const uint32_t e = uint32_t(t[(lo >> (8 * b)) & 0xFu]) ^ uint32_t(t[16 + ((hi >> (8 * b)) & 0xFu)]);
-    p |= e << (8 * b);
-  }
-  return p;
+// The north star's LDS nibble-table kernel.  c*x = T_lo[x & 15] ^ T_hi[x >> 4]
+// with T_lo[v] = c*v, T_hi[v] = c*(v << 4) (galois.h's multiplication
+// restricted to one nibble), staged once per workgroup in LDS.  One LDS
+// entry per (source j, nibble half h, nibble value v) packs the products of
+// ALL R <= 4 output rows -- byte r = coef[r][j] * (v << 4h) -- so a single
+// ds_read_b32 serves every row of a byte's nibble: 8 reads per source dword
+// for all rows together (the round-1 form read one byte per row per nibble:
+// 8 * R ds_read_u8, LDS-issue-bound at 3.7 TB/s).  Zero and unit
+// coefficients are just table contents (branch-free).  The lookup address is
+// the nibble times 4 extracted by one v_perm from a pre-shifted copy of the
+// source dword (the table offset j*128 + 64h is the ds_read immediate); the
+// lo/hi entries fold into per-byte-position accumulators with XOR3, and
+// only at the end does a 4x4 byte transpose (8 v_perm per dword for R = 4)
+// turn "byte position b holds all rows" into "row r holds all positions".
+// A 16-entry table of 4-B entries spans 16 distinct banks: no conflicts.
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+
+__device__ __forceinline__ uint32_t lds_word(lds_u8* base, uint32_t byte_off) {
+  return *(lds_u32*)(base + byte_off);  // C cast: byte address -> dword load (ds_read_b32)
 }
 
 template <int K, int R>
 __global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lut[R * K * 32];
-  for (int i = threadIdx.x; i < R * K * 2; i += kBlock)
-    reinterpret_cast<u32x4*>(lut)[i] = reinterpret_cast<const u32x4*>(a.ntab)[i];
+  __shared__ __attribute__((aligned(16))) uint32_t lut[K * 32];  // [j][h][v]
+  // entry (j, h, v): byte r = coef[r][j] * (v << 4h), from the per-coefficient
+  // nibble tables ntab[r][j] = {c*v (16 B), c*(v << 4) (16 B)}
+  for (int i = threadIdx.x; i < K * 32; i += kBlock) {
+    const int j = i >> 5, hv = i & 31;
+    uint32_t e = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) e |= uint32_t(a.ntab[(r * K + j) * 32 + hv]) << (8 * r);
+    lut[i] = e;
+  }
   __syncthreads();
 
   const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
@@ -666,28 +684,40 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
 #pragma unroll
   for (int j = 0; j < K; ++j) x[j] = load16t<1>(sp[j], col);
 
-  u32x4 acc[R];
+  lds_u8* lb = (lds_u8*)lut;  // C cast: generic -> LDS address space
+  uint32_t e[4][4];  // [dword c][byte position b]: byte r = row r's product byte
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
-
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) e[c][b] = 0u;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    const u32x4 v = x[j];
-    const u32x4 lo = v & 0x0F0F0F0Fu, hi = (v >> 4) & 0x0F0F0F0Fu;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint32_t q0 = a.qtab[r * K + j].x;
-      if (q0 == 0u) continue;
-      if (q0 == kQ0Unit) {
-        acc[r] ^= v;
-        continue;
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t xl = (x[j][c] & 0x0F0F0F0Fu) << 2;  // lo nibble * 4 per byte
+      const uint32_t xh = (x[j][c] >> 2) & 0x3C3C3C3Cu;  // hi nibble * 4 per byte
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        // byte b alone into byte 0 (selector 0x0C = zero byte): one v_perm per address
+        const uint32_t sel = 0x0C0C0C00u | uint32_t(b);
+        const uint32_t lo = lds_word(lb, __builtin_amdgcn_perm(xl, xl, sel) + uint32_t(j * 128));
+        const uint32_t hi = lds_word(lb, __builtin_amdgcn_perm(xh, xh, sel) + uint32_t(j * 128 + 64));
+        e[c][b] = xor3(e[c][b], lo, hi);
       }
-      const uint8_t* t = lut + (r * K + j) * 32;
-      acc[r].x ^= gf_mul_lds(t, lo.x, hi.x);
-      acc[r].y ^= gf_mul_lds(t, lo.y, hi.y);
-      acc[r].z ^= gf_mul_lds(t, lo.z, hi.z);
-      acc[r].w ^= gf_mul_lds(t, lo.w, hi.w);
     }
+  }
+  u32x4 acc[R];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    // 4x4 byte transpose: row r of dword c = byte r of e[c][0..3]
+    const uint32_t p01l = __builtin_amdgcn_perm(e[c][1], e[c][0], 0x05010400u);  // E0.0 E1.0 E0.1 E1.1
+    const uint32_t p23l = __builtin_amdgcn_perm(e[c][3], e[c][2], 0x05010400u);
+    const uint32_t p01h = __builtin_amdgcn_perm(e[c][1], e[c][0], 0x07030602u);  // E0.2 E1.2 E0.3 E1.3
+    const uint32_t p23h = __builtin_amdgcn_perm(e[c][3], e[c][2], 0x07030602u);
+    acc[0][c] = __builtin_amdgcn_perm(p23l, p01l, 0x05040100u);
+    if constexpr (R > 1) acc[1][c] = __builtin_amdgcn_perm(p23l, p01l, 0x07060302u);
+    if constexpr (R > 2) acc[2][c] = __builtin_amdgcn_perm(p23h, p01h, 0x05040100u);
+    if constexpr (R > 3) acc[3][c] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);

@@ -173,11 +173,11 @@ ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p);
  * copies (first touch) or XORs, anything else multiplies (first touch) or
  * multiply-XORs.  Only the block crosses PCIe per arrival; parity is read
  * out once with ecgpu_accum_read.  ecgpu_accum_add is synchronous;
- * ecgpu_accum_add_async only queues the block's copy (copy stream, two
- * device block slots) and its update (compute stream), so the next block's
- * H2D overlaps this block's update -- its block must stay valid and unchanged
- * until ecgpu_accum_sync, a read, a reset or a synchronous add returns (each
- * of which waits for every queued add). */
+ * ecgpu_accum_add_async only queues the block's copy and its update on the
+ * accumulator's own stream and returns, so consecutive blocks cross PCIe back
+ * to back with no host round trip per block -- its block must stay valid and
+ * unchanged until ecgpu_accum_sync, a read, a reset or a synchronous add
+ * returns (each of which waits for every queued add). */
 typedef struct ecgpu_accum ecgpu_accum;
 ECGPU_API ecgpu_accum* ecgpu_accum_create(int m, int64_t size, int device);
 ECGPU_API int ecgpu_accum_add(ecgpu_accum* a, const char* block, const int* coefs /* m */);

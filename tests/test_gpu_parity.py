@@ -592,6 +592,47 @@ def test_host_pipeline_stripe_slab(ec, gpu, restatement, pinned, pitch_pad):
     assert torch.equal(slab, want)
 
 
+@pytest.mark.parametrize("size", [20000, 100003, (2 << 20) + 5])  # zero-copy / bounce / HIP-copy staging
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("pitch_pad", [0, 4099])
+def test_sync_calls_on_host_stripe_slab(ec, gpu, restatement, size, pinned, pitch_pad):
+    """The synchronous drop-in names on shards laid out in one host slab
+    (contiguous or padded rows, pageable or pinned): every staging mode of a
+    host call -- zero-copy for small calls, the pinned bounce, HIP's copies
+    with 2-D runs -- for encode, a decode with non-adjacent erased rows
+    (data, data, parity) and RAID-6, against the oracle; nothing is written
+    past any shard."""
+    import torch
+    k, m = 10, 4
+    pitch = size + pitch_pad
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    slab = torch.zeros((k + m, pitch), dtype=torch.uint8)
+    if pinned:
+        slab = slab.pin_memory()
+    g = torch.Generator().manual_seed(size + pitch_pad + pinned)
+    slab[:k, :size] = torch.randint(0, 256, (k, size), dtype=torch.uint8, generator=g)
+    rows = [slab[i] for i in range(k + m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, rows[:k], rows[k:], size)
+    hd = alloc_shards(k, size, PAD)
+    for j in range(k):
+        hd[j][:size] = slab[j, :size].numpy()
+    ref = _encode_ref(restatement, k, m, M, hd, size)
+    for i in range(m):
+        assert np.array_equal(slab[k + i, :size].numpy(), ref[i][:size]), i
+    assert not slab[:, size:].any()
+    want = slab.clone()
+    er = [1, 6, k + 2]
+    slab[er, :size] = 0
+    assert ec.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, er, rows[:k], rows[k:], size) == 0
+    assert torch.equal(slab, want)
+    slab[k:] = 0
+    assert ec.reed_sol.reed_sol_r6_encode(k, 8, rows[:k], rows[k:k + 2], size) == 1
+    ref6 = _encode_ref(restatement, k, 2, ec.reed_sol.reed_sol_r6_coding_matrix(k, 8), hd, size)
+    for i in range(2):
+        assert np.array_equal(slab[k + i, :size].numpy(), ref6[i][:size]), i
+    assert not slab[:, size:].any() and not slab[k + 2:].any()
+
+
 @pytest.mark.parametrize("erasures", [[0], [0, 1, 2, 3], [2, 11], [10, 13], []])
 def test_host_pipeline_decoder_matches_reference_decode(ec, gpu, erasures):
     import torch

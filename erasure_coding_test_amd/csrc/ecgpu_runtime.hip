@@ -101,15 +101,16 @@ hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t 
 // means fewer DRAM pages open at once across the chip: with each lane reading
 // K shards and writing R, the uncapped kernel (VGPR-limited to 7 blocks/CU)
 // keeps ~28k distinct 4 KiB shard chunks in flight.  What matters is the
-// number of shard streams per CU, blocks x (K + R): about 40 is best
-// (profiles/r01_residency_streams.json): RS(10,4) encode (14
-// streams) and decode{0} (11) at 3 blocks/CU (+9 % on decode{0} vs
-// uncapped), RS(6,3) (9 streams) at 4 (+6 % vs 3), never fewer than 3.  A
-// launch dense in GF multiplies (decode{0,1,2,3}: 40 non-unit coefficients
-// over 14 shards) needs the occupancy to hide its VALU work and loses 7 %,
-// so such launches stay uncapped (cap_for).  The cap is an unused dynamic
-// LDS allocation of LDS_per_CU / blocks (rounded down to 512 B).
-// ECGPU_BLOCKS_PER_CU fixes the block count (0 = never cap).
+// number of shard streams per lane, K + R: a sweep over eight encode and
+// decode shapes (K + R = 5..16, 64 KiB..16 MiB shards, 3 interleaved rounds,
+// profiles/r02_residency_sweep.json) has 4 blocks/CU best or within 0.3 % of
+// the best for K + R <= 9 and 3 blocks/CU for K + R >= 10; never capping is
+// the worst or near it everywhere (-1.5 % to -7 %).  A launch dense in GF
+// multiplies (decode{0,1,2,3}: 40 non-unit coefficients over 14 shards)
+// needs the occupancy to hide its VALU work and loses 7 %, so such launches
+// stay uncapped (cap_for).  The cap is an unused dynamic LDS allocation of
+// LDS_per_CU / blocks (rounded down to 512 B).  ECGPU_BLOCKS_PER_CU fixes the
+// block count (0 = never cap).
 unsigned residency_lds_bytes(int device, int streams) {
   static std::once_flag once;
   static int per_cu = 0;
@@ -119,7 +120,7 @@ unsigned residency_lds_bytes(int device, int streams) {
       per_cu = 0;
     fixed = env_int("ECGPU_BLOCKS_PER_CU", -1);
   });
-  const int blocks = fixed >= 0 ? fixed : std::max(3, 40 / std::max(1, streams));
+  const int blocks = fixed >= 0 ? fixed : (streams <= 9 ? 4 : 3);
   if (blocks <= 0 || per_cu <= 0) return 0;
   const unsigned b = unsigned(per_cu / blocks) & ~511u;
   return b > unsigned(per_cu / (blocks + 1)) ? b : 0u;

@@ -6,8 +6,8 @@
 // ECX datanode (ecx_datanode_main.cpp:714, :724, :1391) link this library in
 // place of src/erasure_coding/*.cpp.  The w = 8 hot path -- matrix encode,
 // decode, dot product, region multiply / XOR, parity, RAID-6 -- runs on the
-// MI355X through include/ecgpu.h; a GPU failure is fatal (message + abort),
-// never a silent CPU fallback.  The w = 16 / 32 region and matrix calls run
+// MI355X through include/ecgpu.h; a GPU failure takes the reference's own
+// failure channel (see gpu_fatal), never a silent CPU fallback.  The w = 16 / 32 region and matrix calls run
 // on the MI355X too (wide-word kernels) when the size is a whole number of
 // words -- the reference's own precondition (jerasure.h: size a multiple of
 // sizeof(long)); a ragged size, where the reference reads and writes past the
@@ -31,9 +31,15 @@
 
 namespace {
 
+// A GPU failure surfaces through the reference's OWN failure channels, never
+// a silent CPU fallback: calls that return a status report it there
+// (jerasure_matrix_decode returns -1, which the client already handles,
+// client_main.cpp:2118-2124); void calls print a message and exit(1), the
+// reference's convention for unrecoverable conditions (galois.cpp:330-334,
+// jerasure.cpp:291-294).
 [[noreturn]] void gpu_fatal(const char* fn, int rc) {
   std::fprintf(stderr, "%s: MI355X path failed (%d): %s\n", fn, rc, ecgpu_last_error());
-  std::abort();
+  std::exit(1);
 }
 
 inline void check(const char* fn, int rc) {
@@ -153,7 +159,10 @@ int jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int
     return ecgpu_cpu::matrix_decode(k, m, w, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size);
   const int rc = ecgpu_jerasure_matrix_decode(k, m, w, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size);
   if (rc == ECGPU_ERR) return -1;
-  check("jerasure_matrix_decode", rc);
+  if (rc != ECGPU_OK) {  // the reference's failure result, with the reason on stderr
+    std::fprintf(stderr, "jerasure_matrix_decode: MI355X path failed (%d): %s\n", rc, ecgpu_last_error());
+    return -1;
+  }
   return 0;
 }
 

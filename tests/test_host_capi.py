@@ -149,7 +149,10 @@ NO_GPU = not os.path.exists("/dev/kfd")
 @pytest.mark.skipif(not NO_GPU, reason="checks the no-GPU failure mode")
 def test_hot_path_without_gpu_fails_loudly():
     """No silent success and no CPU fallback: with no GPU every hot-path call
-    returns ECGPU_ERR_HIP with a message, and the drop-in aborts."""
+    returns ECGPU_ERR_HIP with a message; through the drop-in names a void
+    call exits 1 with the message (the reference's convention,
+    galois.cpp:330-334) and jerasure_matrix_decode returns -1 (its own
+    failure result, which the client handles, client_main.cpp:2118-2124)."""
     from erasure_coding_test_amd import _native as N
     a = np.arange(64, dtype=np.uint8)
     b = np.zeros(64, np.uint8)
@@ -168,7 +171,21 @@ def test_hot_path_without_gpu_fails_loudly():
             "a = np.zeros(64, np.uint8)\n"
             "f(a.ctypes.data, a.ctypes.data, a.ctypes.data, 64)\n")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
-    assert r.returncode != 0 and "MI355X path failed" in r.stderr
+    assert r.returncode == 1 and "MI355X path failed" in r.stderr
+    code = ("import ctypes, numpy as np\n"
+            f"L = ctypes.CDLL({os.path.join(os.path.dirname(N.LIB_PATH), 'libjerasure_amd.so')!r})\n"
+            "vdm = L._Z34reed_sol_vandermonde_coding_matrixiii\n"
+            "vdm.restype = ctypes.c_void_p\n"
+            "M = vdm(4, 2, 8)\n"
+            "dec = L._Z22jerasure_matrix_decodeiiiPiiS_PPcS1_i\n"
+            "bufs = [np.zeros(64, np.uint8) for _ in range(6)]\n"
+            "P = ctypes.c_void_p * 6\n"
+            "ptrs = P(*[b.ctypes.data for b in bufs])\n"
+            "er = (ctypes.c_int * 2)(0, -1)\n"
+            "rc = dec(4, 2, 8, ctypes.c_void_p(M), 0, er, ptrs, ctypes.byref(ptrs, 4 * 8), 64)\n"
+            "print('rc', rc)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "rc -1" in r.stdout and "MI355X path failed" in r.stderr, (r.stdout, r.stderr)
 
 
 def test_int_array_accepts_any_iterable():

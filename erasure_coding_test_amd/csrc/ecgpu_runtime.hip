@@ -216,6 +216,8 @@ struct ecgpu_plan {
   int device = 0, rows = 0, nsrc = 0, w = 8;
   int kind = ECGPU_KERNEL_PERM, nt = 1;
   std::vector<uint32_t> coef;  // host copy, rows x nsrc
+  // one device allocation for all coefficient tables, carved below
+  uint8_t* d_tabs = nullptr;
   u32x4* d_q = nullptr;
   uint32_t* d_p3 = nullptr;   // 3-bit-slice tables, kP3Words per coefficient
   uint8_t* d_nib = nullptr;
@@ -225,9 +227,11 @@ struct ecgpu_plan {
   int stripes = 0;
   int64_t size = 0;
   bool aligned = true;
+  // one device allocation for the pointer tables: sources, then destinations
+  void** d_ptrs = nullptr;
+  size_t cap_ptrs = 0;
   const uint8_t** d_src = nullptr;
   uint8_t** d_dst = nullptr;
-  size_t cap_src = 0, cap_dst = 0;
 };
 
 namespace {
@@ -247,14 +251,8 @@ struct DeviceGuard {
 void plan_free(ecgpu_plan* p) {
   if (!p) return;
   DeviceGuard g(p->device);
-  if (p->d_q) (void)hipFree(p->d_q);
-  if (p->d_p3) (void)hipFree(p->d_p3);
-  if (p->d_nib) (void)hipFree(p->d_nib);
-  if (p->d_w) (void)hipFree(p->d_w);
-  if (p->d_wcls) (void)hipFree(p->d_wcls);
-  if (p->d_wnib) (void)hipFree(p->d_wnib);
-  if (p->d_src) (void)hipFree(p->d_src);
-  if (p->d_dst) (void)hipFree(p->d_dst);
+  if (p->d_tabs) (void)hipFree(p->d_tabs);
+  if (p->d_ptrs) (void)hipFree(p->d_ptrs);
   delete p;
 }
 
@@ -279,13 +277,18 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
       build_wide_tables(p->coef[i], w / 8, &t[i * size_t(nw)]);
       build_wide_nib_tables(p->coef[i], w, &nib[i * size_t(dev::kNibWords)]);
     }
+    // [wide tables | nibble tables | classes] in one allocation, one upload
+    const size_t tb = t.size() * sizeof(uint32_t), nb = nib.size() * sizeof(uint32_t);
+    std::vector<uint8_t> host(tb + nb + n);
+    std::memcpy(host.data(), t.data(), tb);
+    std::memcpy(host.data() + tb, nib.data(), nb);
+    std::memcpy(host.data() + tb + nb, cls.data(), n);
     DeviceGuard g(device);
-    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_w), t.size() * sizeof(uint32_t)));
-    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_wcls), n));
-    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_wnib), nib.size() * sizeof(uint32_t)));
-    ECGPU_HIP(hipMemcpy(p->d_w, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    ECGPU_HIP(hipMemcpy(p->d_wcls, cls.data(), n, hipMemcpyHostToDevice));
-    ECGPU_HIP(hipMemcpy(p->d_wnib, nib.data(), nib.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_tabs), host.size()));
+    ECGPU_HIP(hipMemcpy(p->d_tabs, host.data(), host.size(), hipMemcpyHostToDevice));
+    p->d_w = reinterpret_cast<uint32_t*>(p->d_tabs);
+    p->d_wnib = reinterpret_cast<uint32_t*>(p->d_tabs + tb);
+    p->d_wcls = p->d_tabs + tb + nb;
     return ECGPU_OK;
   }
   for (size_t i = 0; i < n; ++i) p->coef[i] = uint32_t(coefs[i]) & 0xFFu;
@@ -293,13 +296,19 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
   std::vector<uint32_t> p3(n * dev::kP3Words);
   std::vector<uint8_t> nib(n * 32);
   for (size_t i = 0; i < n; ++i) build_tables(coefs[i], &q[i], &p3[i * dev::kP3Words], &nib[i * 32]);
+  // [2-bit tables | 3-bit tables | nibble tables] in one allocation, ONE
+  // upload (three blocking copies cost ~12 us each, tools/hip_overheads.cpp)
+  const size_t qb = n * sizeof(u32x4), pb = p3.size() * sizeof(uint32_t), nb = n * 32;
+  std::vector<uint8_t> host(qb + pb + nb);
+  std::memcpy(host.data(), q.data(), qb);
+  std::memcpy(host.data() + qb, p3.data(), pb);
+  std::memcpy(host.data() + qb + pb, nib.data(), nb);
   DeviceGuard g(device);
-  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_q), n * sizeof(u32x4)));
-  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_p3), p3.size() * sizeof(uint32_t)));
-  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_nib), n * 32));
-  ECGPU_HIP(hipMemcpy(p->d_q, q.data(), n * sizeof(u32x4), hipMemcpyHostToDevice));
-  ECGPU_HIP(hipMemcpy(p->d_p3, p3.data(), p3.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-  ECGPU_HIP(hipMemcpy(p->d_nib, nib.data(), n * 32, hipMemcpyHostToDevice));
+  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_tabs), host.size()));
+  ECGPU_HIP(hipMemcpy(p->d_tabs, host.data(), host.size(), hipMemcpyHostToDevice));
+  p->d_q = reinterpret_cast<u32x4*>(p->d_tabs);
+  p->d_p3 = reinterpret_cast<uint32_t*>(p->d_tabs + qb);
+  p->d_nib = p->d_tabs + qb + pb;
   return ECGPU_OK;
 }
 
@@ -310,28 +319,33 @@ int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* co
               hipStream_t stream, bool keep_alive = false) {
   const size_t ns = size_t(stripes) * p->nsrc, nd = size_t(stripes) * p->rows;
   DeviceGuard g(p->device);
-  if (ns > p->cap_src) {
-    if (p->d_src) ECGPU_HIP(hipFree(p->d_src));
-    p->d_src = nullptr;
-    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_src), ns * sizeof(void*)));
-    p->cap_src = ns;
+  if (ns + nd > p->cap_ptrs) {
+    if (p->d_ptrs) ECGPU_HIP(hipFree(p->d_ptrs));
+    p->d_ptrs = nullptr;
+    p->cap_ptrs = 0;
+    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_ptrs), (ns + nd) * sizeof(void*)));
+    p->cap_ptrs = ns + nd;
   }
-  if (nd > p->cap_dst) {
-    if (p->d_dst) ECGPU_HIP(hipFree(p->d_dst));
-    p->d_dst = nullptr;
-    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_dst), nd * sizeof(void*)));
-    p->cap_dst = nd;
-  }
+  p->d_src = static_cast<const uint8_t**>(static_cast<void*>(p->d_ptrs));
+  p->d_dst = static_cast<uint8_t**>(static_cast<void*>(p->d_ptrs + ns));
   bool aligned = true;
   for (size_t i = 0; i < ns; ++i) aligned &= (reinterpret_cast<uintptr_t>(src[i]) & 15u) == 0;
   for (size_t i = 0; i < nd; ++i) aligned &= (reinterpret_cast<uintptr_t>(dst[i]) & 15u) == 0;
-  if (stream) {
+  if (stream && keep_alive) {
+    // the caller's arrays outlive the stream sync: no wait here
     ECGPU_HIP(hipMemcpyAsync(p->d_src, src, ns * sizeof(void*), hipMemcpyHostToDevice, stream));
     ECGPU_HIP(hipMemcpyAsync(p->d_dst, dst, nd * sizeof(void*), hipMemcpyHostToDevice, stream));
-    if (!keep_alive) ECGPU_HIP(hipStreamSynchronize(stream));  // host tables may die after return
   } else {
-    ECGPU_HIP(hipMemcpy(p->d_src, src, ns * sizeof(void*), hipMemcpyHostToDevice));
-    ECGPU_HIP(hipMemcpy(p->d_dst, dst, nd * sizeof(void*), hipMemcpyHostToDevice));
+    // one upload of [sources | destinations]
+    std::vector<const void*> host(ns + nd);
+    std::memcpy(host.data(), src, ns * sizeof(void*));
+    std::memcpy(host.data() + ns, dst, nd * sizeof(void*));
+    if (stream) {
+      ECGPU_HIP(hipMemcpyAsync(p->d_ptrs, host.data(), (ns + nd) * sizeof(void*), hipMemcpyHostToDevice, stream));
+      ECGPU_HIP(hipStreamSynchronize(stream));  // the host table dies on return
+    } else {
+      ECGPU_HIP(hipMemcpy(p->d_ptrs, host.data(), (ns + nd) * sizeof(void*), hipMemcpyHostToDevice));
+    }
   }
   p->stripes = stripes;
   p->size = size;
@@ -1016,6 +1030,8 @@ struct ecgpu_accum {
   bool pending = false;  // queued work not yet synchronised
 };
 
+}  // extern "C"
+
 namespace {
 
 // The reference's per-accumulator update (ecx_datanode_main.cpp:699-735) for
@@ -1060,6 +1076,8 @@ int accum_async_init(ecgpu_accum* a) {
 }
 
 }  // namespace
+
+extern "C" {
 
 ECGPU_API ecgpu_accum* ecgpu_accum_create(int m, int64_t size, int device) {
   if (m <= 0 || size < 0) {

@@ -650,6 +650,11 @@ size_t zc_max() {
   return v;
 }
 
+bool zero_copy_pinned() {
+  static const bool v = env_int("ECGPU_ZC_PINNED", 1) != 0;
+  return v;
+}
+
 bool inline_enabled() {
   static const bool v = env_int("ECGPU_INLINE", 1) != 0;
   return v;
@@ -711,6 +716,30 @@ int classify(const void* p, int device, bool* on_device) {
   }
   *on_device = false;
   return ECGPU_OK;
+}
+
+// Host memory the GPU addresses in place -- hipHostMalloc'd, or registered
+// with hipHostRegister -- when [p, p + bytes) lies inside ONE such
+// allocation (HIP's range attributes; a range that leaves it would fault).
+// *dev = the device address of p.
+bool host_mapped(const void* p, size_t bytes, void** dev) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (attr.type != hipMemoryTypeHost) return false;
+  void* start = nullptr;
+  size_t range = 0;
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, hipDeviceptr_t(p)) != hipSuccess ||
+      hipPointerGetAttribute(&range, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, hipDeviceptr_t(p)) != hipSuccess ||
+      hipHostGetDevicePointer(dev, const_cast<void*>(p), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const char* c = static_cast<const char*>(p);
+  const char* s0 = static_cast<const char*>(start);
+  return c >= s0 && bytes <= range && size_t(c - s0) <= range - bytes;
 }
 
 bool is_pinned(const void* p) {
@@ -864,6 +893,19 @@ int execute(const FusedOp& op, int64_t size) {
   const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
   auto buf_index = [&](void* p) { return size_t(std::find(bufs.begin(), bufs.end(), p) - bufs.begin()); };
   const bool inl = inline_ok(op);
+  if (inl && zero_copy_pinned()) {
+    // pinned / registered host buffers are read and written by the kernel in
+    // place over PCIe: no staging copy, no DMA setup, and a call's reads and
+    // writes overlap on the two directions of the link
+    for (size_t i = 0; i < bufs.size(); ++i) {
+      void* d = nullptr;
+      if (staged[i] && host_mapped(bufs[i], size_t(size), &d)) {
+        staged[i] = 0;
+        --nstage;
+        devp[i] = static_cast<uint8_t*>(d);
+      }
+    }
+  }
 
   // --- small calls: zero-copy through coherent pinned memory, one launch ---
   if (inl && nstage > 0 && nstage * size_t(size) <= zc_max()) {
@@ -1134,7 +1176,10 @@ ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int
   bool on_dev = false;
   if (int rc = classify(block, a->device, &on_dev)) return rc;
   const char* src = block;
-  if (!on_dev) {
+  void* mapped = nullptr;
+  if (!on_dev && zero_copy_pinned() && host_mapped(block, size_t(a->size), &mapped)) {
+    src = static_cast<const char*>(mapped);  // pinned: the update kernel reads it in place over PCIe
+  } else if (!on_dev) {
     ECGPU_HIP(hipMemcpyAsync(a->d_blk, block, size_t(a->size), hipMemcpyHostToDevice, a->stream));
     src = reinterpret_cast<const char*>(a->d_blk);
   }

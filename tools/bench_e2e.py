@@ -225,6 +225,30 @@ def dropin_pageable(k=10, m=4, S=4 << 20, reps=5):
             "decode_ms": round(td * 1e3, 2), "decode_ok": bool(np.array_equal(bufs[0], saved))}
 
 
+def dropin_pinned(k=10, m=4, S=4 << 20, reps=10):
+    """Synchronous jerasure_matrix_encode / decode{0} on pinned host buffers
+    (torch pin_memory = hipHostMalloc): the kernel reads and writes them in
+    place (ECGPU_ZC_PINNED, default on) -- no staging DMA."""
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = [torch.randint(0, 256, (S,), dtype=torch.uint8).pin_memory() for _ in range(k)]
+    coding = [torch.zeros(S, dtype=torch.uint8).pin_memory() for _ in range(m)]
+    E.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, S)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        E.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, S)
+    te = (time.perf_counter() - t0) / reps
+    bufs = data + coding
+    saved = bufs[0].clone()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        bufs[0].zero_()
+        E.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, [0], bufs[:k], bufs[k:], S)
+    td = (time.perf_counter() - t0) / reps
+    return {"workload": f"jerasure_matrix_encode/decode{{0}} on pinned host buffers, RS({k},{m}) {S >> 20} MiB, "
+                        f"synchronous", "encode_ms": round(te * 1e3, 3), "encode_data_GiBps": round(k * S / te / GiB, 2),
+            "decode_ms": round(td * 1e3, 3), "decode_ok": bool(torch.equal(bufs[0], saved))}
+
+
 def ecx_accum(k=10, m=4, S=4 << 20, stripes=12):
     """ECX incremental accumulation (ecx_datanode_main.cpp:680-735) through
     ParityAccumulator: per stripe, k synchronous adds (one arriving source
@@ -359,6 +383,8 @@ def main():
              "e2e_read_pipeline_1": lambda: e2e_read_pipeline([0], a.stripes),
              "e2e_read_pipeline_4": lambda: e2e_read_pipeline([0, 1, 2, 3], a.stripes),
              "dropin_pageable": dropin_pageable,
+             "dropin_pinned": dropin_pinned,
+             "dropin_pinned_c2": lambda: dropin_pinned(6, 3, 1 << 20, 50),
              "ecx_accum": ecx_accum,
              "call_latency": call_latency,
              "device_configs": device_configs}

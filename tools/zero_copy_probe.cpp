@@ -86,6 +86,37 @@ int main() {
   CK(hipHostMalloc(reinterpret_cast<void**>(&pinned), 64 << 20, hipHostMallocDefault));
   std::memset(pinned, 5, 64 << 20);
 
+  // 0. what HIP reports for host allocations the GPU can address in place:
+  //    range start / size of the allocation a pointer lies in, device address
+  auto range = [&](const char* name, const void* p) {
+    hipPointerAttribute_t attr;
+    const hipError_t e0 = hipPointerGetAttributes(&attr, p);
+    void* start = nullptr;
+    size_t rsize = 0;
+    const hipError_t e1 = hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p);
+    const hipError_t e2 = hipPointerGetAttribute(&rsize, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p);
+    void* dp = nullptr;
+    const hipError_t e3 = hipHostGetDevicePointer(&dp, const_cast<void*>(p), 0);
+    (void)hipGetLastError();
+    std::printf("{\"probe\": \"range %s\", \"type\": %d, \"rc\": [%d, %d, %d, %d], \"offset_in_range\": %lld, "
+                "\"range_size\": %zu, \"dev_equals_host\": %d}\n",
+                name, e0 == hipSuccess ? int(attr.type) : -1, int(e0), int(e1), int(e2), int(e3),
+                (long long)(static_cast<const char*>(p) - static_cast<const char*>(start)), rsize, int(dp == p));
+    std::fflush(stdout);
+  };
+  range("hipHostMalloc base", pinned);
+  range("hipHostMalloc +12345", pinned + 12345);
+  {
+    char* reg = host + 100003;  // not page aligned
+    CK(hipHostRegister(reg, 3 << 20, hipHostRegisterDefault));
+    range("registered base (unaligned)", reg);
+    range("registered +1 MiB", reg + (1 << 20));
+    range("registered last byte", reg + (3 << 20) - 1);
+    range("just past registered", reg + (3 << 20) + 8192);
+    CK(hipHostUnregister(reg));
+  }
+  range("pageable", host + 12345);
+
   // 1. registration cost on fresh ranges (never registered before)
   size_t off = 0;
   for (size_t n : {size_t(64) << 10, size_t(349525), size_t(1) << 20, size_t(6) << 20, size_t(16) << 20}) {

@@ -470,15 +470,11 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
     int mul_terms = 0;  // coefficients that are neither 0 nor 1
     for (int r = 0; r < R; ++r)
       for (int j = 0; j < K; ++j) mul_terms += p->coef[size_t(r0 + r) * K + j] > 1u;
-    // Engine per launch: the v_perm engine (unit coefficients compiled as
-    // XORs) unless the launch is dense in GF multiplies (> 2.5 per shard
-    // touched, e.g. decode{0,1,2,3}: 40 over 14 shards), where its VALU work
-    // (1018 ops per lane-column) binds and the LDS nibble-table engine (716
-    // ops + 320 ds_read_b32 whatever the coefficients) is faster: C4 0.244 ->
-    // 0.230 ms (profiles/r02_engine_ab.json).  ECGPU_DENSE=0 keeps v_perm.
-    static const bool dense_lds = env_int("ECGPU_DENSE", 1) != 0;
-    const bool dense = 2 * mul_terms > 5 * (K + R);
-    const bool use_lds = p->kind == ECGPU_KERNEL_LDS || (dense_lds && dense);
+    // The v_perm engine unless ECGPU_KERNEL / ecgpu_plan_set_kernel asks for the
+    // LDS nibble-table engine.  (Dense launches on the LDS engine were tried:
+    // an in-process interleaved A/B has v_perm 2.5 % faster on C4 decode
+    // {0,1,2,3} and even on RS(12,4) {0,1,2,3}, profiles/r02_engine_ab_inprocess.json.)
+    const bool use_lds = p->kind == ECGPU_KERNEL_LDS;
     KernelFn vec_fn = spec ? spec_kernel(use_lds, K, R, unit_variant(p->coef, K, r0, R), p->nt) : generic_fn(R);
     const int vec = 1;
     // (the LDS engine runs uncapped: capping it cost 4 % encode, 16 % decode{0})

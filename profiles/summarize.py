@@ -36,7 +36,7 @@ KERNELS = {
     "encode": ("gf_apply<10, 4, 3,", 10 * 4 * MiB * 96, 4 * 4 * MiB * 96),
     "decode": ("gf_apply<10, 1, 4,", 10 * 4 * MiB * 96, 1 * 4 * MiB * 96),
     "C2_encode": ("gf_apply<6, 3, 3,", 6 * MiB * 128, 3 * MiB * 128),
-    "C4_decode_0123": ("gf_apply_lds<10, 4>", 10 * 4 * MiB * 24, 4 * 4 * MiB * 24),  # dense: LDS engine
+    "C4_decode_0123": ("gf_apply<10, 4, 0,", 10 * 4 * MiB * 24, 4 * 4 * MiB * 24),
     "C5_encode": ("gf_apply<12, 4, 3,", 12 * 16 * MiB * 8, 4 * 16 * MiB * 8),
 }
 WORKLOAD_KEY = "C3:96"  # bench.py load_traffic key: --config C3, 96 stripes/GPU

@@ -395,10 +395,20 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
   const bool force_perm = env_int("ECGPU_WIDE", 0) == 1;
   for (int r0 = 0; r0 < p->rows; r0 += dev::kMaxRows) {
     const int R = std::min(dev::kMaxRows, p->rows - r0);
-    const unsigned nib_lds = unsigned(K) * unsigned(dev::nib_source_bytes(R));
+    // w = 16 packs two rows per LDS dword (gf_apply_wide_nib16, half the LDS bytes)
+    const bool pack16 = W == 2 && env_int("ECGPU_NIB16", 1) != 0;
+    const unsigned nib_lds =
+        unsigned(K) * unsigned(pack16 ? dev::nib16_source_bytes(R) : dev::nib_source_bytes(R));
     const bool nib = !force_perm && nib_lds <= unsigned(dev::kNibMaxLds);
     KernelFn vec_fn = nullptr, word_fn = W == 2 ? &dev::gf_apply_wide_words<2> : &dev::gf_apply_wide_words<4>;
-    if (nib) {
+    if (nib && pack16) {
+      switch (R) {
+        case 1: vec_fn = &dev::gf_apply_wide_nib16<1>; break;
+        case 2: vec_fn = &dev::gf_apply_wide_nib16<2>; break;
+        case 3: vec_fn = &dev::gf_apply_wide_nib16<3>; break;
+        default: vec_fn = &dev::gf_apply_wide_nib16<4>; break;
+      }
+    } else if (nib) {
       switch (R) {
         case 1: vec_fn = &dev::gf_apply_wide_nib<1>; break;
         case 2: vec_fn = &dev::gf_apply_wide_nib<2>; break;

@@ -1192,5 +1192,102 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib(ApplyArgs a) {
   }
 }
 
+// w = 16 variant with two rows per LDS dword.  w = 16 products are 16-bit,
+// so one dword entry packs rows 2p and 2p+1: (j, t, v) -> [row 2p | row 2p+1]
+// of c*(v << 4t') for the word that nibble t belongs to (t < 4: low word,
+// t >= 4: high word, t' = t mod 4).  An entry is 4 B for R <= 2 and 8 B for
+// R = 3, 4 -- half of gf_apply_wide_nib's LDS bytes per lookup (that kernel
+// is LDS-bound) -- and the folding works on packed row pairs: per pair one
+// accumulator for the low-word tables, one for the high-word tables (2 XOR3
+// each per source dword, half of the per-row form), and at the end one
+// v_perm per row interleaves them: row 2p = [lo.lo16 | hi.lo16], row 2p+1 =
+// [lo.hi16 | hi.hi16].  The entries are derived in the staging loop from the
+// same per-coefficient tables (a.wtab, [R][K][kNibWords]).
+__host__ __device__ constexpr int nib16_entry_words(int R) { return R <= 2 ? 1 : 2; }
+__host__ __device__ constexpr int nib16_source_bytes(int R) { return kNibWords * 4 * nib16_entry_words(R); }
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
+  constexpr int EW = nib16_entry_words(R), EB = 4 * EW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t nib_lds[];
+  const int K = a.K;
+  const int n = K * kNibWords * EW;
+  for (int i = threadIdx.x; i < n; i += kBlock) {
+    const int pr = i % EW, e = (i / EW) % kNibWords, j = i / (EW * kNibWords);
+    const bool high = (e >> 4) >= 4;  // tables 4..7 hold the high word's products in bits 16..31
+    auto word = [&](int r) -> uint32_t {
+      if (r >= R) return 0u;
+      const uint32_t v = a.wtab[size_t(r * K + j) * kNibWords + e];
+      return high ? (v >> 16) : (v & 0xFFFFu);
+    };
+    reinterpret_cast<uint32_t*>(nib_lds)[i] = word(2 * pr) | (word(2 * pr + 1) << 16);
+  }
+  __syncthreads();
+
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(static_cast<void*>(nib_lds)));
+  constexpr int kChunk = 8;  // source loads in flight before the first use
+  const int64_t nblk = (a.nvec + kBlock - 1) / kBlock;
+  for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const int64_t col = b * kBlock + threadIdx.x;
+    if (col >= a.nvec) continue;
+    uint32_t lo[4][EW], hi[4][EW];  // [dword c][row pair]
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int q = 0; q < EW; ++q) lo[c][q] = hi[c][q] = 0u;
+    for (int j0 = 0; j0 < K; j0 += kChunk) {
+      u32x4 xs[kChunk];
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u)
+        if (j0 + u < K) xs[u] = load16t<1>(sp[j0 + u], col);
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u) {
+        const int j = j0 + u;
+        if (j >= K) break;
+        const uint32_t jbase = lds_base + uint32_t(j) * uint32_t(nib16_source_bytes(R));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t x = xs[u][c];
+          // nibble t of x scaled by EB in byte t/2 of ns[t & 1] (see gf_apply_wide_nib)
+          constexpr int kSh = EB == 8 ? 3 : 2;
+          constexpr uint32_t kNibMask = 0x0F0F0F0Fu << kSh;
+          const uint32_t ns[2] = {(x << kSh) & kNibMask, (x >> (4 - kSh)) & kNibMask};
+          uint32_t v[8][EW];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
+                                uint32_t(t * 16 * EB);
+            if constexpr (EW == 1) {
+              v[t][0] = *(lds_u32*)(size_t(ad));
+            } else {
+              const u32x2 q = *(lds_u32x2*)(size_t(ad));
+              v[t][0] = q.x;
+              v[t][1] = q.y;
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < EW; ++q) {
+            lo[c][q] = xor3(xor3(lo[c][q], v[0][q], v[1][q]), v[2][q], v[3][q]);
+            hi[c][q] = xor3(xor3(hi[c][q], v[4][q], v[5][q]), v[6][q], v[7][q]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      u32x4 o;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        o[c] = __builtin_amdgcn_perm(hi[c][r >> 1], lo[c][r >> 1], (r & 1) ? 0x07060302u : 0x05040100u);
+      store16t<1>(dp[r], col, o);
+    }
+  }
+}
+
 }  // namespace dev
 }  // namespace ecgpu

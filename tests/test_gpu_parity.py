@@ -1113,6 +1113,49 @@ def test_random_fused_maps_vs_reference_table(ec, gpu, vectors, seed):
     p.close()
 
 
+@pytest.mark.parametrize("where", ["device", "host", "pinned"])
+@pytest.mark.parametrize("seed", range(16))
+def test_random_fused_maps_sync_calls(ec, gpu, vectors, seed, where):
+    """The same random maps through the SYNCHRONOUS surface
+    (jerasure_matrix_encode with an arbitrary K x R matrix, one stripe):
+    the inline-argument launches (K <= 16, one launch per 4 rows, the byte
+    path for misaligned buffers), the plan path above 16 sources, and every
+    host staging mode (zero-copy, bounce, HIP copies; pinned in place).  An
+    all-zero row leaves its destination untouched (jerasure.cpp:561-620)."""
+    import torch
+    T = vectors["gf_mul_table"].reshape(256, 256)
+    rng, K, R, _, size, coefs, offs = _random_map_case(seed)
+    src = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(K)]
+    bases, views = [], []
+    for j in range(K + R):
+        o = int(offs[0, j])
+        if where == "device":
+            b = torch.full((o + size + PAD,), 0xCC, dtype=torch.uint8, device=gpu)
+        else:
+            b = torch.full((o + size + PAD,), 0xCC, dtype=torch.uint8)
+            if where == "pinned":
+                b = b.pin_memory()
+        v = b[o:o + size]
+        if j < K:
+            v.copy_(torch.from_numpy(src[j]))
+        bases.append(b)
+        views.append(v if where != "host" else v.numpy())
+    ec.jerasure.jerasure_matrix_encode(K, R, 8, coefs.ravel().tolist(), views[:K], views[K:], size)
+    for r in range(R):
+        b = bases[K + r].cpu().numpy()
+        o = int(offs[0, K + r])
+        if not coefs[r].any():
+            want = np.full(size, 0xCC, np.uint8)
+        else:
+            want = np.zeros(size, np.uint8)
+            for j in range(K):
+                want ^= T[coefs[r, j]][src[j]]
+        assert np.array_equal(b[o:o + size], want), (seed, where, K, R, size, r)
+        assert (b[:o] == 0xCC).all() and (b[o + size:] == 0xCC).all(), "wrote outside the region"
+    for j in range(K):  # sources untouched
+        assert np.array_equal(bases[j].cpu().numpy()[int(offs[0, j]):int(offs[0, j]) + size], src[j])
+
+
 # jerasure_matrix_decode on random (k, m, erasures, row_k_ones) against the
 # reference library compiled from /root/reference (oracle/_ref): decoded
 # bytes must equal the reference decode on the same inputs, and the return

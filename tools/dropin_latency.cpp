@@ -206,6 +206,8 @@ void ecx_case(int k, int m, int block_size, int stripes) {
 
 int main(int argc, char** argv) {
   const bool quick = argc > 1 && std::strcmp(argv[1], "--quick") == 0;
+  // --only PREFIX: the client cases whose name starts with PREFIX, stripe buffer layout only
+  const char* only = argc > 2 && std::strcmp(argv[1], "--only") == 0 ? argv[2] : nullptr;
   const int e0[] = {0};
   const int e0123[] = {0, 1, 2, 3};
   const Case cases[] = {{"default RS(3,3) 1 MiB (ych_ec_test.h)", 3, 3, 1 << 20, 100},
@@ -213,6 +215,11 @@ int main(int argc, char** argv) {
                         {"C2 RS(6,3) 1 MiB", 6, 3, 1 << 20, 100},
                         {"C3 RS(10,4) 4 MiB", 10, 4, 4 << 20, 30},
                         {"C5 RS(12,4) 16 MiB", 12, 4, 16 << 20, quick ? 4 : 10}};
+  if (only) {
+    for (const Case& c : cases)
+      if (std::strncmp(c.name, only, std::strlen(only)) == 0) client_case(c, true, e0, 1);
+    return 0;
+  }
   for (int stripe_buffer = 1; stripe_buffer >= 0; --stripe_buffer)
     for (const Case& c : cases) client_case(c, stripe_buffer != 0, e0, 1);
   client_case({"C4 RS(10,4) 4 MiB", 10, 4, 4 << 20, 30}, true, e0123, 4);

@@ -835,15 +835,29 @@ bool inline_ok(const FusedOp& op) {
          env_int("ECGPU_KERNEL", ECGPU_KERNEL_PERM) == ECGPU_KERNEL_PERM && !(op.dst_is_src && rows > dev::kMaxRows);
 }
 
-// One gf_apply_inl launch per <= 4 output rows over `size` bytes.
+// Workgroups of an inline launch that reads or writes host memory in place
+// (zero-copy): queued 4 MiB pinned reads ran at 52.5 GB/s with 256
+// grid-stride workgroups and 41 GB/s with 1024+ (too many PCIe requests in
+// flight; tools/zero_copy_probe.cpp); through the drop-in, 32-64 workgroups
+// were best (C3 pinned encode 0.83 ms vs 0.93-0.96 uncapped,
+// profiles/r02_zc_grid_sweep.txt).  0 = uncapped.
+int64_t zc_grid() {
+  static const int64_t v = env_int("ECGPU_ZC_GRID", 64);
+  return v;
+}
+
+// One gf_apply_inl launch per <= 4 output rows over `size` bytes.  host_io:
+// some pointer is host memory the kernel reads / writes over PCIe (grid
+// capped at zc_grid()).
 int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, const std::vector<uint8_t*>& dp,
-                  int64_t size, hipStream_t s) {
+                  int64_t size, hipStream_t s, bool host_io) {
   const int K = int(sp.size()), rows = int(dp.size());
   bool aligned = true;
   for (auto* p : sp) aligned &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
   for (auto* p : dp) aligned &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
   const int64_t nvec = aligned ? size / 16 : 0, byte0 = nvec * 16;
-  const int64_t nbv = (nvec + dev::kBlock - 1) / dev::kBlock;
+  int64_t nbv = (nvec + dev::kBlock - 1) / dev::kBlock;
+  if (host_io && zc_grid() > 0) nbv = std::min(nbv, zc_grid());
   const int64_t nbb = (size - byte0 + dev::kBlock - 1) / dev::kBlock;
   for (int r0 = 0; r0 < rows; r0 += dev::kMaxRows) {
     const int R = std::min(dev::kMaxRows, rows - r0);
@@ -899,6 +913,7 @@ int execute(const FusedOp& op, int64_t size) {
   const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
   auto buf_index = [&](void* p) { return size_t(std::find(bufs.begin(), bufs.end(), p) - bufs.begin()); };
   const bool inl = inline_ok(op);
+  bool host_io = false;  // some buffer is used in place in host memory
   if (inl && zero_copy_pinned()) {
     // pinned / registered host buffers are read and written by the kernel in
     // place over PCIe: no staging copy, no DMA setup, and a call's reads and
@@ -909,6 +924,7 @@ int execute(const FusedOp& op, int64_t size) {
         staged[i] = 0;
         --nstage;
         devp[i] = static_cast<uint8_t*>(d);
+        host_io = true;
       }
     }
   }
@@ -924,7 +940,7 @@ int execute(const FusedOp& op, int64_t size) {
     std::vector<const uint8_t*> sp(devp.begin(), devp.begin() + nsrc);
     std::vector<uint8_t*> dp(static_cast<size_t>(rows));
     for (int r = 0; r < rows; ++r) dp[size_t(r)] = devp[buf_index(op.dsts[size_t(r)])];
-    if (int rc = launch_inline(op, sp, dp, size, c->stream)) return rc;
+    if (int rc = launch_inline(op, sp, dp, size, c->stream, /*host_io=*/true)) return rc;
     ECGPU_HIP(hipStreamSynchronize(c->stream));
     ECGPU_HIP(hipGetLastError());
     for (int r = 0; r < rows; ++r) {
@@ -969,7 +985,7 @@ int execute(const FusedOp& op, int64_t size) {
     // add, galois.cpp:447-451): nothing to read.
     for (int r = 0; r < rows; ++r) ECGPU_HIP(hipMemsetAsync(dp[r], 0, size_t(size), c->stream));
   } else if (inl) {
-    if ((rc = launch_inline(op, sp, dp, size, c->stream)) != ECGPU_OK) return rc;
+    if ((rc = launch_inline(op, sp, dp, size, c->stream, host_io)) != ECGPU_OK) return rc;
   } else {
     ecgpu_plan* p = nullptr;
     rc = ctx_plan(c, rows, nsrc, op.coef, op.w, &p);
@@ -1183,8 +1199,10 @@ ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int
   if (int rc = classify(block, a->device, &on_dev)) return rc;
   const char* src = block;
   void* mapped = nullptr;
+  bool in_place = false;
   if (!on_dev && zero_copy_pinned() && host_mapped(block, size_t(a->size), &mapped)) {
     src = static_cast<const char*>(mapped);  // pinned: the update kernel reads it in place over PCIe
+    in_place = true;
   } else if (!on_dev) {
     ECGPU_HIP(hipMemcpyAsync(a->d_blk, block, size_t(a->size), hipMemcpyHostToDevice, a->stream));
     src = reinterpret_cast<const char*>(a->d_blk);
@@ -1197,7 +1215,7 @@ ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int
     for (void* p : op.srcs) sp.push_back(static_cast<const uint8_t*>(p));
     std::vector<uint8_t*> dp;
     for (void* p : op.dsts) dp.push_back(static_cast<uint8_t*>(p));
-    if (int rc = launch_inline(op, sp, dp, a->size, a->stream)) return rc;
+    if (int rc = launch_inline(op, sp, dp, a->size, a->stream, /*host_io=*/in_place)) return rc;
   } else {
     // engine override or > 4 aliased rows: the synchronous path
     if (int rc = accum_sync(a)) return rc;

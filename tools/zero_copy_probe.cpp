@@ -193,6 +193,46 @@ int main() {
                 n, us, double(2 * n) / (us * 1e3), double(n) / (us * 1e3));
     std::fflush(stdout);
   }
+  // 4. queued back-to-back 4 MiB reads of pinned memory (the ECX accumulator's
+  //    per-block traffic): kernel reads at several grid sizes / words in
+  //    flight per lane vs DMA, 20 in a row, one sync at the end
+  {
+    const size_t n = size_t(4) << 20;
+    const int reps = 20;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto queued = [&](const char* name, auto&& one) {
+      for (int w = 0; w < 3; ++w) one();
+      CK(hipStreamSynchronize(s));
+      std::vector<double> t;
+      for (int r = 0; r < 5; ++r) {
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < reps; ++i) one();
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t.push_back(double(ms) * 1e3 / reps);
+      }
+      const double us = median(t);
+      std::printf("{\"probe\": \"queued 4 MiB pinned read: %s\", \"us_per_block\": %.2f, \"GBps\": %.1f}\n", name, us,
+                  double(n) / (us * 1e3));
+      std::fflush(stdout);
+    };
+    const int64_t n16 = int64_t(n / 16);
+    for (int grid : {256, 512, 1024, 2048, 4096}) {
+      char name[64];
+      std::snprintf(name, sizeof(name), "kernel grid %d x 256", grid);
+      queued(name, [&] {
+        hipLaunchKernelGGL(copy16, dim3(grid), dim3(256), 0, s, reinterpret_cast<const u32x4*>(pinned),
+                           reinterpret_cast<u32x4*>(dev), n16);
+      });
+    }
+    queued("DMA hipMemcpyAsync", [&] { CK(hipMemcpyAsync(dev, pinned, n, hipMemcpyHostToDevice, s)); });
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+  }
   CK(hipHostFree(pinned));
   CK(hipFree(dev));
   std::free(host);

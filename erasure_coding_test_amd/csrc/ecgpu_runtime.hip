@@ -1883,8 +1883,9 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
   for (auto* p : sb) aligned &= (reinterpret_cast<uintptr_t>(p) & 7u) == 0;
   for (auto* p : db) aligned &= (reinterpret_cast<uintptr_t>(p) & 7u) == 0;
   // 16-B lanes when everything is 16-B aligned; ECGPU_PACKET=1 forces 8-B
-  // lanes (A/B, RS(10,4) w = 8 64 MiB bit-matrix encode on MI355X: 16-B lanes
-  // with 8 source rows in flight 186 us, 4 in flight 198, 8-B lanes 190)
+  // lanes, 2 the unpipelined 16-B kernel (A/B, RS(10,4) w = 8 64 MiB
+  // bit-matrix encode on MI355X: pipelined 16-B lanes 180.5 us, unpipelined
+  // with 8 rows in flight 187, 8-B lanes 190; profiles/r02_packet_ab.txt)
   const int packet_kind = env_int("ECGPU_PACKET", 0);
   bool wide16 = aligned && packet_kind != 1 && ps % 16 == 0 && spstride % 16 == 0 && dstride % 16 == 0;
   for (auto* p : sb) wide16 &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
@@ -1908,10 +1909,14 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
       continue;
     }
     void* fn = nullptr;
-    if (wide16)
+    if (wide16 && packet_kind == 2)
       fn = R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets16<8, 8>)
            : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets16<16, 8>)
                      : reinterpret_cast<void*>(&dev::gf_xor_packets16<32, 8>);
+    else if (wide16)
+      fn = R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets16p<8>)
+           : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets16p<16>)
+                     : reinterpret_cast<void*>(&dev::gf_xor_packets16p<32>);
     else
       fn = aligned ? (R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets<8>)
                       : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets<16>)

@@ -893,19 +893,23 @@ def test_wide_word_region_ops_device(ec, gpu, w):
 
 
 # ------------------------------------------ GF(2) bit-matrix / schedules ----
-def _np_bitmatrix_encode(k, m, w, bm, data, size, ps):
-    """Plain numpy restatement of jerasure_bitmatrix_encode (jerasure.cpp:301-345)."""
-    out = [np.zeros(size, np.uint8) for _ in range(m)]
+def _np_bitmatrix_encode(k, m, w, bm, data, size, ps, init=None):
+    """Plain numpy restatement of jerasure_bitmatrix_encode (jerasure.cpp:301-345):
+    an output packet whose bit-matrix row is all zero is left as it was
+    (`init`, zeros by default) -- the reference only memcpy's / XORs."""
+    out = [np.zeros(size, np.uint8) if init is None else init[i].copy() for i in range(m)]
     for i in range(m):
         for sp in range(0, size, w * ps):
             for j in range(w):
-                acc = np.zeros(ps, np.uint8)
+                acc = None
                 row = bm[(i * w + j) * k * w:(i * w + j + 1) * k * w]
                 for x in range(k):
                     for y in range(w):
                         if row[x * w + y]:
-                            acc ^= data[x][sp + y * ps:sp + (y + 1) * ps]
-                out[i][sp + j * ps:sp + (j + 1) * ps] = acc
+                            src = data[x][sp + y * ps:sp + (y + 1) * ps]
+                            acc = src.copy() if acc is None else acc ^ src
+                if acc is not None:
+                    out[i][sp + j * ps:sp + (j + 1) * ps] = acc
     return out
 
 
@@ -939,6 +943,31 @@ def test_bitmatrix_coding_device(ec, gpu, k, m, w, ps):
     torch.cuda.synchronize()
     for j in range(k):
         assert np.array_equal(dd[j].cpu().numpy(), data[j]), j
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), want[i]), i
+
+
+@pytest.mark.parametrize("kind", ["0", "1", "2"])  # ECGPU_PACKET: pipelined 16-B, 8-B lanes, unpipelined 16-B
+@pytest.mark.parametrize("k,m,w,ps", [(1, 1, 3, 64), (5, 2, 3, 128), (3, 2, 5, 16), (10, 4, 8, 2048),
+                                      (7, 5, 2, 48), (4, 3, 3, 8), (3, 3, 3, 5)])
+def test_random_bitmatrix_packet_kernels(ec, gpu, monkeypatch, kind, k, m, w, ps):
+    """A random 0/1 bit-matrix (any w) through jerasure_bitmatrix_encode on
+    every packet kernel: source-row counts below one pipelined chunk of four
+    (k*w = 3), with a ragged tail (15), and whole chunks (80); 16-B, 8-B and
+    byte packets; more than 8 / 16 output rows; all-zero rows leave their
+    output packets untouched, as the reference does."""
+    import torch
+    monkeypatch.setenv("ECGPU_PACKET", kind)
+    rng = np.random.default_rng(k * 131 + m * 17 + w * 5 + ps)
+    bm = [int(b) for b in rng.integers(0, 2, k * w * m * w)]
+    size = w * ps * 7
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)]
+    init = [np.full(size, 0x5A, np.uint8) for _ in range(m)]
+    want = _np_bitmatrix_encode(k, m, w, bm, data, size, ps, init)
+    dd = [torch.from_numpy(a).to(gpu) for a in data]
+    dc = [torch.from_numpy(a).to(gpu) for a in init]
+    ec.jerasure.jerasure_bitmatrix_encode(k, m, w, bm, dd, dc, size, ps)
+    torch.cuda.synchronize()
     for i in range(m):
         assert np.array_equal(dc[i].cpu().numpy(), want[i]), i
 

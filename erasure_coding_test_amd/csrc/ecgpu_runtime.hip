@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <list>
 #include <map>
@@ -1277,6 +1278,24 @@ struct ecgpu_pipeline {
   int64_t next_ticket = 0;
   int64_t done_below = 0;             // every ticket < done_below has completed
   std::mutex mu;
+  // D2H worker (pipeline_d2h_worker): HIP's pageable copies block the
+  // thread that issues them, so a stripe's D2H into pageable buffers is
+  // issued by this thread while the submitting thread already moves the next
+  // stripe's H2D -- the two directions of the link overlap.  Pinned outputs
+  // are issued inline when no job is pending (their copies do not block).
+  struct D2HJob {
+    int slot;
+    int64_t ticket;
+    std::vector<char*> hp;
+  };
+  std::thread worker;
+  std::mutex qmu;
+  std::condition_variable qcv;
+  std::deque<D2HJob> q;
+  int64_t issued_below = 0;  // every ticket < issued_below has its D2H enqueued (drained event recorded)
+  bool stop = false;
+  int worker_rc = 0;  // ECGPU_OK, or the first failure of a worker-issued D2H
+  std::string worker_err;
 
   int nsrc() const { return int(src_ids.size()); }
   int rows() const { return int(out_ids.size()); }
@@ -1288,6 +1307,14 @@ struct ecgpu_pipeline {
 namespace {
 void pipeline_free(ecgpu_pipeline* p) {
   if (!p) return;
+  if (p->worker.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(p->qmu);
+      p->stop = true;
+    }
+    p->qcv.notify_all();
+    p->worker.join();
+  }
   DeviceGuard g(p->device);
   for (auto* pl : p->plans) plan_free(pl);
   for (auto& v : {&p->loaded, &p->computed, &p->drained})
@@ -1302,6 +1329,12 @@ void pipeline_free(ecgpu_pipeline* p) {
 int pipeline_retire(ecgpu_pipeline* p, int slot) {
   const int64_t t = p->slot_ticket[slot];
   if (t < 0) return ECGPU_OK;
+  {
+    // the slot's drained event is only meaningful once its D2H is enqueued
+    std::unique_lock<std::mutex> lk(p->qmu);
+    p->qcv.wait(lk, [&] { return p->issued_below > t; });
+    if (p->worker_rc != ECGPU_OK) return fail(p->worker_rc, p->worker_err);
+  }
   ECGPU_HIP(hipEventSynchronize(p->drained[slot]));
   p->slot_ticket[slot] = -1;
   // tickets complete in submission order (the D2H stream is in order)
@@ -1389,9 +1422,53 @@ ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create_decode(int k, int m, int w, cons
 
 
 namespace {
+bool pipe_d2h_worker_enabled() {
+  static const bool v = env_int("ECGPU_PIPE_D2H_WORKER", 1) != 0;
+  return v;
+}
+
+// D2H of a slot's outputs to the host pointers hp (s_d2h, after the slot's
+// compute), then the slot's drained event.
+int pipeline_d2h(ecgpu_pipeline* p, int sl, const std::vector<char*>& hp) {
+  ECGPU_HIP(hipStreamWaitEvent(p->s_d2h, p->computed[sl], 0));
+  if (int rc = copy_shards(false, p->slot_shard(sl, p->nsrc()), p->slot_stride, hp, size_t(p->size), p->s_d2h))
+    return rc;
+  ECGPU_HIP(hipEventRecord(p->drained[sl], p->s_d2h));
+  return ECGPU_OK;
+}
+
+void pipeline_d2h_worker(ecgpu_pipeline* p) {
+  (void)hipSetDevice(p->device);  // once: this thread only ever drives this device
+  for (;;) {
+    ecgpu_pipeline::D2HJob job;
+    {
+      std::unique_lock<std::mutex> lk(p->qmu);
+      p->qcv.wait(lk, [&] { return p->stop || !p->q.empty(); });
+      if (p->q.empty()) return;  // stop, nothing left
+      job = std::move(p->q.front());
+      p->q.pop_front();
+    }
+    int rc = ECGPU_OK;
+    bool failed_before = false;
+    {
+      std::lock_guard<std::mutex> lk(p->qmu);
+      failed_before = p->worker_rc != ECGPU_OK;
+    }
+    if (!failed_before) rc = pipeline_d2h(p, job.slot, job.hp);
+    std::lock_guard<std::mutex> lk(p->qmu);
+    if (rc != ECGPU_OK && p->worker_rc == ECGPU_OK) {
+      p->worker_rc = rc;
+      p->worker_err = t_err;
+    }
+    p->issued_below = job.ticket + 1;
+    p->qcv.notify_all();
+  }
+}
+
 // Queues stripe t into ring slot t % depth: H2D of the sources (s_h2d), the
-// fused apply (s_comp), D2H of the outputs (s_d2h).
-int pipeline_enqueue(ecgpu_pipeline* p, int sl, char** data_ptrs, char** coding_ptrs) {
+// fused apply (s_comp), then D2H of the outputs (s_d2h) -- issued here, or
+// by the pipeline's D2H worker when an output is pageable.
+int pipeline_enqueue(ecgpu_pipeline* p, int sl, int64_t t, char** data_ptrs, char** coding_ptrs) {
   auto host = [&](int id) { return id < p->k ? data_ptrs[id] : coding_ptrs[id - p->k]; };
   const int ns = p->nsrc(), nr = p->rows();
   const size_t bytes = size_t(p->size);
@@ -1410,11 +1487,24 @@ int pipeline_enqueue(ecgpu_pipeline* p, int sl, char** data_ptrs, char** coding_
       ECGPU_HIP(hipMemsetAsync(p->slot_shard(sl, ns + i), 0, bytes, p->s_comp));
   }
   ECGPU_HIP(hipEventRecord(p->computed[sl], p->s_comp));
-  ECGPU_HIP(hipStreamWaitEvent(p->s_d2h, p->computed[sl], 0));
   hp.clear();
   for (int i = 0; i < nr; ++i) hp.push_back(host(p->out_ids[i]));
-  if ((rc = copy_shards(false, p->slot_shard(sl, ns), p->slot_stride, hp, bytes, p->s_d2h)) != ECGPU_OK) return rc;
-  ECGPU_HIP(hipEventRecord(p->drained[sl], p->s_d2h));
+  bool pageable = false;
+  for (char* h : hp) pageable = pageable || !is_pinned(h);
+  std::unique_lock<std::mutex> lk(p->qmu);
+  if (p->worker_rc != ECGPU_OK) return fail(p->worker_rc, p->worker_err);
+  if ((pageable && pipe_d2h_worker_enabled()) || !p->q.empty()) {
+    // behind any pending job, so s_d2h keeps submission order
+    if (!p->worker.joinable()) p->worker = std::thread(pipeline_d2h_worker, p);
+    p->q.push_back(ecgpu_pipeline::D2HJob{sl, t, std::move(hp)});
+    lk.unlock();
+    p->qcv.notify_all();
+    return ECGPU_OK;
+  }
+  lk.unlock();
+  if ((rc = pipeline_d2h(p, sl, hp)) != ECGPU_OK) return rc;
+  lk.lock();
+  p->issued_below = t + 1;
   return ECGPU_OK;
 }
 }  // namespace
@@ -1427,7 +1517,7 @@ ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, cha
   const int sl = int(t % p->depth);
   int rc = pipeline_retire(p, sl);  // the slot's previous stripe must be out
   if (rc != ECGPU_OK) return rc;
-  rc = pipeline_enqueue(p, sl, data_ptrs, coding_ptrs);
+  rc = pipeline_enqueue(p, sl, t, data_ptrs, coding_ptrs);
   if (rc != ECGPU_OK) {
     // part of the stripe may already be queued against the caller's buffers:
     // let it finish before reporting, so no DMA outlives the failed call

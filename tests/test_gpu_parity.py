@@ -552,6 +552,34 @@ def test_host_pipeline_matches_oracle(ec, gpu, restatement, memory):
                 ec.pipeline.host_unregister(b)
 
 
+@pytest.mark.parametrize("pattern", ["alternate", "pageable_then_pinned"])
+def test_host_pipeline_mixed_output_memory(ec, gpu, restatement, pattern):
+    """Pageable outputs go through the pipeline's D2H worker thread, pinned
+    ones inline unless a worker job is pending: stripes switching between the
+    two keep submission order (depth 2 reuses slots while jobs are queued),
+    and close() with stripes in flight drains them."""
+    import torch
+    k, m, size, stripes = 6, 3, (1 << 20) + 16, 9
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = [host_shards(70, s, k, size) for s in range(stripes)]
+
+    def pinned_at(s):
+        return s % 2 == 1 if pattern == "alternate" else s >= stripes // 2
+
+    coding = [[torch.full((size + PAD,), 0x77, dtype=torch.uint8).pin_memory() for _ in range(m)] if pinned_at(s)
+              else [np.full(size + PAD, 0x77, np.uint8) for _ in range(m)] for s in range(stripes)]
+    p = ec.HostPipeline(k, m, M, size, depth=2)
+    tickets = [p.submit(data[s], coding[s]) for s in range(stripes)]
+    p.wait(tickets[3])
+    p.close()  # stripes 4.. still in flight
+    for s in range(stripes):
+        ref = _encode_ref(restatement, k, m, M, data[s], size)
+        for i in range(m):
+            got = coding[s][i].numpy() if hasattr(coding[s][i], "numpy") else coding[s][i]
+            assert np.array_equal(got[:size], ref[i][:size]), (s, i)
+            assert (got[size:] == 0x77).all(), (s, i)
+
+
 @pytest.mark.parametrize("pinned", [True, False])
 @pytest.mark.parametrize("pitch_pad", [0, 4096 + 3])
 def test_host_pipeline_stripe_slab(ec, gpu, restatement, pinned, pitch_pad):

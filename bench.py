@@ -408,7 +408,9 @@ def load_traffic(name: str, workload_key: str):
 
 def config_block(E, N, dev, stream, kind, nt, main=None):
     """Every BASELINE.json GPU config as its own launch (median of 20 HIP-event
-    timed launches after warm-up, ≥ 1 GiB streamed per launch): C2 encode,
+    timed launches after warm-up; batches sized to 4.5-6.5 GB streamed per
+    launch, like the timed C3 steps' 5.6 GB, so launch ramp and tail weigh
+    the same in every config): C2 encode,
     C3 encode / decode{0} (from the timed steps), C4 decode{0,1,2,3} with its
     host-side plan cost reported separately, C5 encode."""
     import ctypes
@@ -429,11 +431,11 @@ def config_block(E, N, dev, stream, kind, nt, main=None):
         p.close()
         del slab, shards
 
-    encode_cfg("C2_encode", 6, 3, 1 << 20, 128, 2)
+    encode_cfg("C2_encode", 6, 3, 1 << 20, 512, 2)
     if main is not None:
         out.update(main)
     # C4: worst-case decode, erasures {0,1,2,3} of RS(10,4) 4 MiB (10 survivors = ids 4..13)
-    k, m, S, B = 10, 4, 4 << 20, 24
+    k, m, S, B = 10, 4, 4 << 20, 96
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     slab, shards = E.alloc_stripes(B, k, m, S, dev)
     fill_random(slab, list(range(B)), 4)
@@ -470,7 +472,7 @@ def config_block(E, N, dev, stream, kind, nt, main=None):
     out["C4_decode_0123"] = e
     dp.close()
     del slab, shards
-    encode_cfg("C5_encode", 12, 4, 16 << 20, 8, 5)
+    encode_cfg("C5_encode", 12, 4, 16 << 20, 24, 5)
     torch.cuda.synchronize(dev)
     return out
 

@@ -14,8 +14,8 @@ largest grid of that kernel name) are averaged, so the bench's one-stripe
 self-check launches are excluded.
 
 Kernels: every launch shape of the default bench line -- the timed C3 encode
-and decode{0} (96 stripes) and the configs block's C2 encode (128 stripes),
-C4 decode{0,1,2,3} (24 stripes) and C5 encode (8 stripes).
+and decode{0} (96 stripes) and the configs block's C2 encode (512 stripes),
+C4 decode{0,1,2,3} (96 stripes) and C5 encode (24 stripes).
 
     python profiles/summarize.py --tag r02 --trace gpurun_out/prof_trace \
         --fetch gpurun_out/prof_fetch --write gpurun_out/prof_write
@@ -35,9 +35,9 @@ MiB = 1 << 20
 KERNELS = {
     "encode": ("gf_apply<10, 4, 3,", 10 * 4 * MiB * 96, 4 * 4 * MiB * 96),
     "decode": ("gf_apply<10, 1, 4,", 10 * 4 * MiB * 96, 1 * 4 * MiB * 96),
-    "C2_encode": ("gf_apply<6, 3, 3,", 6 * MiB * 128, 3 * MiB * 128),
-    "C4_decode_0123": ("gf_apply<10, 4, 0,", 10 * 4 * MiB * 24, 4 * 4 * MiB * 24),
-    "C5_encode": ("gf_apply<12, 4, 3,", 12 * 16 * MiB * 8, 4 * 16 * MiB * 8),
+    "C2_encode": ("gf_apply<6, 3, 3,", 6 * MiB * 512, 3 * MiB * 512),
+    "C4_decode_0123": ("gf_apply<10, 4, 0,", 10 * 4 * MiB * 96, 4 * 4 * MiB * 96),
+    "C5_encode": ("gf_apply<12, 4, 3,", 12 * 16 * MiB * 24, 4 * 16 * MiB * 24),
 }
 WORKLOAD_KEY = "C3:96"  # bench.py load_traffic key: --config C3, 96 stripes/GPU
 

@@ -657,6 +657,22 @@ size_t zc_max() {
   return v;
 }
 
+// A call above bounce_max() whose staged outputs total at most zc_out_max()
+// bytes, each at most zc_out_shard_max(), has the kernel write its outputs
+// into coherent pinned memory (see execute).  A pageable D2H costs 67 us per
+// 1 MiB shard but runs at link rate from 4 MiB (86 us): drop-in C2 encode 333
+// -> 296 us, C3 decode{0} (one 4 MiB output) 871 -> 1005 us if it took this
+// path (profiles/r02_zc_out_ab.txt).
+size_t zc_out_max() {
+  static const size_t v = size_t(env_int("ECGPU_ZC_OUT_KIB", 4096)) << 10;
+  return v;
+}
+
+size_t zc_out_shard_max() {
+  static const size_t v = size_t(env_int("ECGPU_ZC_OUT_SHARD_KIB", 1024)) << 10;
+  return v;
+}
+
 bool zero_copy_pinned() {
   static const bool v = env_int("ECGPU_ZC_PINNED", 1) != 0;
   return v;
@@ -949,6 +965,51 @@ int execute(const FusedOp& op, int64_t size) {
       if (staged[i]) std::memcpy(op.dsts[size_t(r)], devp[i], size_t(size));
     }
     return ECGPU_OK;
+  }
+
+  // --- larger calls with few output bytes: sources cross by HIP's copies
+  // (a contiguous pageable run goes as one pinned blit at link rate), the
+  // kernel writes the outputs straight into coherent pinned memory and the
+  // calling thread copies them out: no per-output pageable D2H (67 us per
+  // 1 MiB shard, tools/pageable_duplex_probe.cpp).  Outputs that are also
+  // sources keep the staged path.
+  if (inl && nstage > 0 && nstage * slot > bounce_max()) {
+    size_t nout = 0;
+    bool aliased = false;
+    std::vector<char> is_out(bufs.size(), 0);
+    for (int r = 0; r < rows; ++r) {
+      const size_t i = buf_index(op.dsts[size_t(r)]);
+      if (!staged[i] || is_out[i]) continue;
+      is_out[i] = 1;
+      aliased = aliased || i < size_t(nsrc);
+      ++nout;
+    }
+    if (!aliased && nout > 0 && nout * size_t(size) <= zc_out_max() && size_t(size) <= zc_out_shard_max()) {
+      const size_t nin = nstage - nout;
+      if (int rc = ensure_zc(c, nout * slot)) return rc;
+      if (int rc = ensure_stage(c, std::max<size_t>(nin, 1) * slot)) return rc;
+      size_t ni = 0, no = 0;
+      std::vector<char*> staged_hp;
+      for (size_t i = 0; i < bufs.size(); ++i) {
+        if (!staged[i]) continue;
+        if (is_out[i]) {
+          devp[i] = c->zc + (no++) * slot;
+        } else {
+          devp[i] = c->stage + (ni++) * slot;
+          staged_hp.push_back(static_cast<char*>(bufs[i]));
+        }
+      }
+      if (int rc = copy_shards(true, c->stage, slot, staged_hp, size_t(size), c->stream)) return rc;
+      std::vector<const uint8_t*> sp(devp.begin(), devp.begin() + nsrc);
+      std::vector<uint8_t*> dp(static_cast<size_t>(rows));
+      for (int r = 0; r < rows; ++r) dp[size_t(r)] = devp[buf_index(op.dsts[size_t(r)])];
+      if (int rc = launch_inline(op, sp, dp, size, c->stream, /*host_io=*/true)) return rc;
+      ECGPU_HIP(hipStreamSynchronize(c->stream));
+      ECGPU_HIP(hipGetLastError());
+      for (size_t i = 0; i < bufs.size(); ++i)
+        if (staged[i] && is_out[i]) std::memcpy(bufs[i], devp[i], size_t(size));
+      return ECGPU_OK;
+    }
   }
 
   // With several launches (> 4 rows) an output that is also a source must

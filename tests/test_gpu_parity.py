@@ -620,10 +620,12 @@ def test_host_pipeline_stripe_slab(ec, gpu, restatement, pinned, pitch_pad):
     assert torch.equal(slab, want)
 
 
-# zero-copy / bounce / HIP-copy staging; (3 << 20) + 48 keeps every row 16-B
-# aligned when unpadded, so pinned rows run the vector columns grid-stride
-# over a capped grid (ECGPU_ZC_GRID) with a partial last sweep
-@pytest.mark.parametrize("size", [20000, 100003, (2 << 20) + 5, (3 << 20) + 48])
+# zero-copy / bounce / HIP-copy staging; 600001 and 655360 stage more than the
+# bounce limit with outputs <= 1 MiB each (sources by HIP's copies, outputs
+# written by the kernel into coherent pinned memory); (3 << 20) + 48 keeps
+# every row 16-B aligned when unpadded, so pinned rows run the vector columns
+# grid-stride over a capped grid (ECGPU_ZC_GRID) with a partial last sweep
+@pytest.mark.parametrize("size", [20000, 100003, 600001, 655360, (2 << 20) + 5, (3 << 20) + 48])
 @pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("pitch_pad", [0, 4099])
 def test_sync_calls_on_host_stripe_slab(ec, gpu, restatement, size, pinned, pitch_pad):

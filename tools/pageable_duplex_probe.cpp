@@ -104,6 +104,32 @@ int main() {
   bench("D2H 4 x 4 MiB, blocking hipMemcpy", [&] {
     for (int i = 0; i < m; ++i) CK(hipMemcpy(hout[i], dev + (k + i) * S, S, hipMemcpyDeviceToHost));
   });
+  // does a pageable range that once was an H2D source take a faster D2H path?
+  for (size_t n : {size_t(1) << 20, size_t(4) << 20}) {
+    char* fresh = static_cast<char*>(std::malloc(n));
+    char* used = static_cast<char*>(std::malloc(n));
+    std::memset(fresh, 0, n);
+    std::memset(used, 0, n);
+    CK(hipMemcpy(dev, used, n, hipMemcpyHostToDevice));
+    char name[96];
+    std::snprintf(name, sizeof(name), "D2H %zu KiB into a buffer never copied H2D", n >> 10);
+    bench(name, [&] {
+      CK(hipMemcpyAsync(fresh, dev, n, hipMemcpyDeviceToHost, s_blk));
+      CK(hipStreamSynchronize(s_blk));
+    });
+    std::snprintf(name, sizeof(name), "D2H %zu KiB into a buffer once copied H2D", n >> 10);
+    bench(name, [&] {
+      CK(hipMemcpyAsync(used, dev, n, hipMemcpyDeviceToHost, s_blk));
+      CK(hipStreamSynchronize(s_blk));
+    });
+    std::snprintf(name, sizeof(name), "H2D %zu KiB", n >> 10);
+    bench(name, [&] {
+      CK(hipMemcpyAsync(dev, used, n, hipMemcpyHostToDevice, s_blk));
+      CK(hipStreamSynchronize(s_blk));
+    });
+    std::free(fresh);
+    std::free(used);
+  }
   bench("H2D 10 x 4 MiB alone", h2d);
   bench("D2H 4 x 4 MiB alone", d2h);
   bench("H2D then D2H, one thread", [&] {

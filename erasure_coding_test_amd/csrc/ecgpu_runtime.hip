@@ -1,5 +1,8 @@
 // ecgpu_runtime.hip -- device side of include/ecgpu.h: plans, kernel
-// dispatch, staging of host buffers, and the hot-path C ABI.
+// dispatch, staging of host buffers, and the hot-path C ABI.  The ECX
+// accumulators (accum.hip), host pipelines (pipeline.hip) and GF(2) packet
+// coding (packets.hip) build on the helpers this file exports to them
+// through runtime.hpp.
 //
 // Execution model (MI355X-first, not the reference's byte loops):
 //   * every hot-path call is planned on the host into ONE fused
@@ -37,12 +40,14 @@
 #include "gf_spec.hpp"
 #include "matrix_host.hpp"
 #include "planner.hpp"
+#include "runtime.hpp"
 
 using namespace ecgpu;
+using namespace ecgpu::rt;
 using dev::ApplyArgs;
 using dev::u32x4;
 
-namespace {
+ECGPU_RT_BEGIN
 
 thread_local std::string t_err;
 
@@ -51,12 +56,6 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
-#define ECGPU_HIP(expr)                                                                          \
-  do {                                                                                           \
-    hipError_t e_ = (expr);                                                                      \
-    if (e_ != hipSuccess)                                                                        \
-      return fail(ECGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
-  } while (0)
 
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -210,44 +209,10 @@ void build_wide_nib_tables(uint32_t c, int w, uint32_t* t) {
 
 int wide_words_per_coef(int w) { return w == 16 ? 2 * dev::Wide<2>::kPerms : 2 * dev::Wide<4>::kPerms; }
 
-}  // namespace
+ECGPU_RT_END
 
-// ----------------------------------------------------------------- plan ----
-struct ecgpu_plan {
-  int device = 0, rows = 0, nsrc = 0, w = 8;
-  int kind = ECGPU_KERNEL_PERM, nt = 1;
-  std::vector<uint32_t> coef;  // host copy, rows x nsrc
-  // one device allocation for all coefficient tables, carved below
-  uint8_t* d_tabs = nullptr;
-  u32x4* d_q = nullptr;
-  uint32_t* d_p3 = nullptr;   // 3-bit-slice tables, kP3Words per coefficient
-  uint8_t* d_nib = nullptr;
-  uint32_t* d_w = nullptr;     // wide-word tables (w = 16 / 32)
-  uint8_t* d_wcls = nullptr;   // wide coefficient classes
-  uint32_t* d_wnib = nullptr;  // wide-word LDS nibble tables, kNibWords per coefficient
-  int stripes = 0;
-  int64_t size = 0;
-  bool aligned = true;
-  // one device allocation for the pointer tables: sources, then destinations
-  void** d_ptrs = nullptr;
-  size_t cap_ptrs = 0;
-  const uint8_t** d_src = nullptr;
-  uint8_t** d_dst = nullptr;
-};
+ECGPU_RT_BEGIN
 
-namespace {
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
 
 void plan_free(ecgpu_plan* p) {
   if (!p) return;
@@ -257,7 +222,7 @@ void plan_free(ecgpu_plan* p) {
   delete p;
 }
 
-int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, int w = 8) {
+int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, int w) {
   p->device = device;
   p->rows = rows;
   p->nsrc = nsrc;
@@ -317,7 +282,7 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
 // `keep_alive` (the caller keeps src/dst alive until it synchronises the
 // stream, as execute() does) the call waits for the upload.
 int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* const* dst, int64_t size,
-              hipStream_t stream, bool keep_alive = false) {
+              hipStream_t stream, bool keep_alive) {
   const size_t ns = size_t(stripes) * p->nsrc, nd = size_t(stripes) * p->rows;
   DeviceGuard g(p->device);
   if (ns + nd > p->cap_ptrs) {
@@ -533,23 +498,6 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
 }
 
 // ------------------------------------------------------ context pool ----
-struct PlanKey {
-  int rows, nsrc, w;
-  std::vector<uint32_t> coef;
-  bool operator==(const PlanKey& o) const { return rows == o.rows && nsrc == o.nsrc && w == o.w && coef == o.coef; }
-};
-
-struct Ctx {
-  int device = -1;
-  hipStream_t stream = nullptr;
-  uint8_t* stage = nullptr;
-  size_t stage_cap = 0;
-  uint8_t* bounce = nullptr;  // pinned host mirror of the staging slab (mid-size calls, see execute)
-  size_t bounce_cap = 0;
-  uint8_t* zc = nullptr;      // coherent pinned memory the kernel reads / writes in place (small calls)
-  size_t zc_cap = 0;
-  std::list<std::pair<PlanKey, ecgpu_plan*>> plans;  // LRU, front = newest
-};
 
 std::mutex g_pool_mu;
 std::vector<Ctx*> g_pool;  // idle contexts; never destroyed (process lifetime)
@@ -596,14 +544,6 @@ void release_ctx(Ctx* c) {
   g_pool.push_back(c);
 }
 
-struct CtxLease {
-  int rc = ECGPU_OK;  // declared first: initialised before acquire_ctx writes it
-  Ctx* c = nullptr;
-  explicit CtxLease(int device) : c(acquire_ctx(device, &rc)) {}
-  ~CtxLease() {
-    if (c) release_ctx(c);
-  }
-};
 
 int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int w, ecgpu_plan** out) {
   PlanKey key{rows, nsrc, w, coef};
@@ -1097,8 +1037,7 @@ int execute(const FusedOp& op, int64_t size) {
   return ECGPU_OK;
 }
 
-}  // namespace
-
+ECGPU_RT_END
 // ================================================================ C ABI ====
 extern "C" {
 
@@ -1139,659 +1078,6 @@ ECGPU_API int ecgpu_plan_launch(ecgpu_plan* p, void* stream) {
 }
 
 ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p) { plan_free(p); }
-
-// ---------------------------------------------------- ECX accumulators ----
-struct ecgpu_accum {
-  int device = 0, m = 0;
-  int64_t size = 0;
-  size_t slot = 0;
-  uint8_t* d_acc = nullptr;  // m slots, each `slot` bytes (skewed shard stride)
-  std::vector<char> init;
-  // queued adds (ecgpu_accum_add_async): a host block is copied into the
-  // device block buffer and applied, both on the accumulator's own stream,
-  // and the call returns; the copy of block j+1 queues behind the update of
-  // block j (stream order protects the buffer) with no host round trip
-  uint8_t* d_blk = nullptr;
-  hipStream_t stream = nullptr;
-  bool pending = false;  // queued work not yet synchronised
-};
-
-}  // extern "C"
-
-namespace {
-
-// The reference's per-accumulator update (ecx_datanode_main.cpp:699-735) for
-// one arriving block as ONE fused op: coefficient 0 leaves an accumulator
-// alone, 1 copies (first touch) or XORs, any other multiplies (first touch)
-// or multiply-adds.
-FusedOp accum_op(ecgpu_accum* a, const char* block, const int* coefs) {
-  LinearTracker t;
-  char* src = const_cast<char*>(block);
-  for (int i = 0; i < a->m; ++i) {
-    const int c = coefs[i] & 0xFF;
-    if (c == 0) continue;
-    char* acc = ecgpu_accum_device_ptr(a, i);
-    if (c == 1) {
-      if (a->init[i])
-        t.xor3(src, acc, acc);
-      else
-        t.copy(acc, src);
-    } else {
-      t.mul(src, c, acc, a->init[i] != 0);
-    }
-  }
-  return t.finish();
-}
-
-int accum_sync(ecgpu_accum* a) {
-  if (!a->pending) return ECGPU_OK;
-  ECGPU_HIP(hipStreamSynchronize(a->stream));
-  ECGPU_HIP(hipGetLastError());
-  a->pending = false;
-  return ECGPU_OK;
-}
-
-int accum_async_init(ecgpu_accum* a) {
-  if (a->stream) return ECGPU_OK;
-  DeviceGuard g(a->device);
-  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&a->d_blk), a->slot));
-  // a blocking stream: ordered after the caller's null-stream work like every
-  // synchronous call (a device-resident block filled by PyTorch, say)
-  ECGPU_HIP(hipStreamCreateWithFlags(&a->stream, hipStreamDefault));
-  return ECGPU_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-ECGPU_API ecgpu_accum* ecgpu_accum_create(int m, int64_t size, int device) {
-  if (m <= 0 || size < 0) {
-    fail(ECGPU_ERR_ARG, "ecgpu_accum_create: m > 0 and size >= 0 required");
-    return nullptr;
-  }
-  auto* a = new ecgpu_accum();
-  a->device = device < 0 ? current_device() : device;
-  a->m = m;
-  a->size = size;
-  a->slot = size_t(ecgpu_recommended_shard_stride(size));
-  a->init.assign(size_t(m), 0);
-  DeviceGuard g(a->device);
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(&a->d_acc), a->slot * size_t(m));
-  if (e != hipSuccess) {
-    fail(ECGPU_ERR_HIP, std::string("ecgpu_accum_create: ") + hipGetErrorString(e));
-    delete a;
-    return nullptr;
-  }
-  return a;
-}
-
-ECGPU_API char* ecgpu_accum_device_ptr(ecgpu_accum* a, int i) {
-  if (!a || i < 0 || i >= a->m) return nullptr;
-  return reinterpret_cast<char*>(a->d_acc + size_t(i) * a->slot);
-}
-
-ECGPU_API int ecgpu_accum_add(ecgpu_accum* a, const char* block, const int* coefs) {
-  if (!a || !block || !coefs) return fail(ECGPU_ERR_ARG, "ecgpu_accum_add: bad arguments");
-  if (int rc = accum_sync(a)) return rc;  // after every earlier asynchronous add
-  DeviceGuard g(a->device);
-  const int rc = execute(accum_op(a, block, coefs), a->size);
-  if (rc != ECGPU_OK) return rc;
-  for (int i = 0; i < a->m; ++i)
-    if (coefs[i] & 0xFF) a->init[i] = 1;
-  return ECGPU_OK;
-}
-
-// Queued add: the block's H2D copy (host blocks, into the device block
-// buffer) and its fused update go onto the accumulator's stream and the
-// call returns, so consecutive blocks stream over PCIe back to back with no
-// host round trip per block.  (A second copy stream overlapping block j+1's
-// H2D with block j's ~6 us update measured slower: the cross-stream event
-// waits cost more than the overlap buys)  The block must stay
-// valid and unchanged until ecgpu_accum_sync (or a read, a reset, a
-// synchronous add) returns.
-ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int* coefs) {
-  if (!a || !block || !coefs) return fail(ECGPU_ERR_ARG, "ecgpu_accum_add_async: bad arguments");
-  bool any = false;
-  for (int i = 0; i < a->m; ++i) any |= (coefs[i] & 0xFF) != 0;
-  if (!any || a->size == 0) return ECGPU_OK;
-  if (int rc = accum_async_init(a)) return rc;
-  DeviceGuard g(a->device);
-  bool on_dev = false;
-  if (int rc = classify(block, a->device, &on_dev)) return rc;
-  const char* src = block;
-  void* mapped = nullptr;
-  bool in_place = false;
-  if (!on_dev && zero_copy_pinned() && host_mapped(block, size_t(a->size), &mapped)) {
-    src = static_cast<const char*>(mapped);  // pinned: the update kernel reads it in place over PCIe
-    in_place = true;
-  } else if (!on_dev) {
-    ECGPU_HIP(hipMemcpyAsync(a->d_blk, block, size_t(a->size), hipMemcpyHostToDevice, a->stream));
-    src = reinterpret_cast<const char*>(a->d_blk);
-  }
-  a->pending = true;
-  const FusedOp op = accum_op(a, src, coefs);
-  if (inline_ok(op)) {
-    add_stats(op);
-    std::vector<const uint8_t*> sp;
-    for (void* p : op.srcs) sp.push_back(static_cast<const uint8_t*>(p));
-    std::vector<uint8_t*> dp;
-    for (void* p : op.dsts) dp.push_back(static_cast<uint8_t*>(p));
-    if (int rc = launch_inline(op, sp, dp, a->size, a->stream, /*host_io=*/in_place)) return rc;
-  } else {
-    // engine override or > 4 aliased rows: the synchronous path
-    if (int rc = accum_sync(a)) return rc;
-    if (int rc = execute(op, a->size)) return rc;
-  }
-  for (int i = 0; i < a->m; ++i)
-    if (coefs[i] & 0xFF) a->init[i] = 1;
-  return ECGPU_OK;
-}
-
-ECGPU_API int ecgpu_accum_sync(ecgpu_accum* a) {
-  if (!a) return fail(ECGPU_ERR_ARG, "ecgpu_accum_sync: null");
-  return accum_sync(a);
-}
-
-ECGPU_API int ecgpu_accum_read(ecgpu_accum* a, int i, char* out, int64_t nbytes) {
-  if (!a || i < 0 || i >= a->m || !out || nbytes < 0 || nbytes > a->size)
-    return fail(ECGPU_ERR_ARG, "ecgpu_accum_read: bad arguments");
-  if (int rc = accum_sync(a)) return rc;
-  if (!a->init[i]) return ECGPU_ERR;
-  DeviceGuard g(a->device);
-  if (a->stream) {  // on the accumulator's own stream, not the device-wide null stream
-    ECGPU_HIP(hipMemcpyAsync(out, ecgpu_accum_device_ptr(a, i), size_t(nbytes), hipMemcpyDefault, a->stream));
-    ECGPU_HIP(hipStreamSynchronize(a->stream));
-  } else {
-    ECGPU_HIP(hipMemcpy(out, ecgpu_accum_device_ptr(a, i), size_t(nbytes), hipMemcpyDefault));
-  }
-  return ECGPU_OK;
-}
-
-ECGPU_API int ecgpu_accum_reset(ecgpu_accum* a) {
-  if (!a) return fail(ECGPU_ERR_ARG, "ecgpu_accum_reset: null");
-  if (int rc = accum_sync(a)) return rc;
-  std::fill(a->init.begin(), a->init.end(), 0);
-  return ECGPU_OK;
-}
-
-ECGPU_API void ecgpu_accum_destroy(ecgpu_accum* a) {
-  if (!a) return;
-  (void)accum_sync(a);
-  DeviceGuard g(a->device);
-  if (a->stream) (void)hipStreamDestroy(a->stream);
-  if (a->d_blk) (void)hipFree(a->d_blk);
-  if (a->d_acc) (void)hipFree(a->d_acc);
-  delete a;
-}
-
-// ---------------------------------------------------- host pipeline ----
-struct ecgpu_pipeline {
-  int device = 0, k = 0, m = 0, depth = 0;
-  int64_t size = 0;
-  std::vector<int> src_ids, out_ids;  // shard ids read / written (id < k: data_ptrs[id], else coding_ptrs[id-k])
-  size_t slot_stride = 0;             // bytes between shards inside a ring slot
-  uint8_t* d_ring = nullptr;          // depth slots x (nsrc inputs, then rows outputs)
-  std::vector<ecgpu_plan*> plans;     // one bound plan per ring slot (none when nsrc or rows is 0)
-  hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
-  std::vector<hipEvent_t> loaded, computed, drained;
-  std::vector<int64_t> slot_ticket;  // ticket occupying each slot (-1: free)
-  int64_t next_ticket = 0;
-  int64_t done_below = 0;             // every ticket < done_below has completed
-  std::mutex mu;
-  // D2H worker (pipeline_d2h_worker): HIP's pageable copies block the
-  // thread that issues them, so a stripe's D2H into pageable buffers is
-  // issued by this thread while the submitting thread already moves the next
-  // stripe's H2D -- the two directions of the link overlap.  Pinned outputs
-  // are issued inline when no job is pending (their copies do not block).
-  struct D2HJob {
-    int slot;
-    int64_t ticket;
-    std::vector<char*> hp;
-  };
-  std::thread worker;
-  std::mutex qmu;
-  std::condition_variable qcv;
-  std::deque<D2HJob> q;
-  int64_t issued_below = 0;  // every ticket < issued_below has its D2H enqueued (drained event recorded)
-  bool stop = false;
-  int worker_rc = 0;  // ECGPU_OK, or the first failure of a worker-issued D2H
-  std::string worker_err;
-
-  int nsrc() const { return int(src_ids.size()); }
-  int rows() const { return int(out_ids.size()); }
-  uint8_t* slot_shard(int slot, int j) const {
-    return d_ring + slot_stride * (size_t(nsrc() + rows()) * size_t(slot) + size_t(j));
-  }
-};
-
-namespace {
-void pipeline_free(ecgpu_pipeline* p) {
-  if (!p) return;
-  if (p->worker.joinable()) {
-    {
-      std::lock_guard<std::mutex> lk(p->qmu);
-      p->stop = true;
-    }
-    p->qcv.notify_all();
-    p->worker.join();
-  }
-  DeviceGuard g(p->device);
-  for (auto* pl : p->plans) plan_free(pl);
-  for (auto& v : {&p->loaded, &p->computed, &p->drained})
-    for (auto e : *v)
-      if (e) (void)hipEventDestroy(e);
-  for (auto s : {p->s_h2d, p->s_comp, p->s_d2h})
-    if (s) (void)hipStreamDestroy(s);
-  if (p->d_ring) (void)hipFree(p->d_ring);
-  delete p;
-}
-
-int pipeline_retire(ecgpu_pipeline* p, int slot) {
-  const int64_t t = p->slot_ticket[slot];
-  if (t < 0) return ECGPU_OK;
-  {
-    // the slot's drained event is only meaningful once its D2H is enqueued
-    std::unique_lock<std::mutex> lk(p->qmu);
-    p->qcv.wait(lk, [&] { return p->issued_below > t; });
-    if (p->worker_rc != ECGPU_OK) return fail(p->worker_rc, p->worker_err);
-  }
-  ECGPU_HIP(hipEventSynchronize(p->drained[slot]));
-  p->slot_ticket[slot] = -1;
-  // tickets complete in submission order (the D2H stream is in order)
-  if (t + 1 > p->done_below) p->done_below = t + 1;
-  return ECGPU_OK;
-}
-
-// rows x nsrc coefficient map from shard ids src_ids to shard ids out_ids.
-ecgpu_pipeline* pipeline_build(int k, int m, int rows, int nsrc, const int* coef, const int* src_ids,
-                               const int* out_ids, int64_t size, int depth, int device) {
-  auto* p = new ecgpu_pipeline();
-  p->device = device < 0 ? current_device() : device;
-  p->k = k;
-  p->m = m;
-  p->depth = depth;
-  p->size = size;
-  p->src_ids.assign(src_ids, src_ids + nsrc);
-  p->out_ids.assign(out_ids, out_ids + rows);
-  p->slot_stride = size_t(ecgpu_recommended_shard_stride(size));
-  DeviceGuard g(p->device);
-  auto bad = [&](hipError_t e, const char* what) {
-    fail(ECGPU_ERR_HIP, std::string("ecgpu_pipeline: ") + what + ": " + hipGetErrorString(e));
-    pipeline_free(p);
-    return static_cast<ecgpu_pipeline*>(nullptr);
-  };
-  hipError_t e = hipSuccess;
-  const size_t ring = p->slot_stride * size_t(nsrc + rows) * size_t(depth);
-  if (ring && (e = hipMalloc(reinterpret_cast<void**>(&p->d_ring), ring)) != hipSuccess) return bad(e, "hipMalloc");
-  for (hipStream_t* s : {&p->s_h2d, &p->s_comp, &p->s_d2h})
-    if ((e = hipStreamCreateWithFlags(s, hipStreamNonBlocking)) != hipSuccess) return bad(e, "stream");
-  for (auto* v : {&p->loaded, &p->computed, &p->drained}) {
-    v->assign(size_t(depth), nullptr);
-    for (auto& ev : *v)
-      if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "event");
-  }
-  p->slot_ticket.assign(size_t(depth), -1);
-  if (nsrc > 0 && rows > 0) {
-    for (int sl = 0; sl < depth; ++sl) {
-      std::vector<const uint8_t*> src(static_cast<size_t>(nsrc));
-      std::vector<uint8_t*> dst(static_cast<size_t>(rows));
-      for (int j = 0; j < nsrc; ++j) src[j] = p->slot_shard(sl, j);
-      for (int i = 0; i < rows; ++i) dst[i] = p->slot_shard(sl, nsrc + i);
-      auto* pl = new ecgpu_plan();
-      if (plan_init(pl, rows, nsrc, coef, p->device) != ECGPU_OK ||
-          plan_bind(pl, 1, src.data(), dst.data(), size, nullptr) != ECGPU_OK) {
-        plan_free(pl);
-        pipeline_free(p);
-        return nullptr;
-      }
-      p->plans.push_back(pl);
-    }
-  }
-  return p;
-}
-}  // namespace
-
-ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create(int k, int m, const int* matrix, int64_t size, int depth,
-                                                int device) {
-  if (k <= 0 || m <= 0 || !matrix || size <= 0 || depth <= 0) {
-    fail(ECGPU_ERR_ARG, "ecgpu_pipeline_create: bad arguments");
-    return nullptr;
-  }
-  std::vector<int> src(static_cast<size_t>(k)), out(static_cast<size_t>(m));
-  for (int j = 0; j < k; ++j) src[j] = j;
-  for (int i = 0; i < m; ++i) out[i] = k + i;
-  return pipeline_build(k, m, m, k, matrix, src.data(), out.data(), size, depth, device);
-}
-
-ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create_decode(int k, int m, int w, const int* matrix, int row_k_ones,
-                                                       const int* erasures, int64_t size, int depth, int device) {
-  if (k <= 0 || m <= 0 || w != 8 || !matrix || !erasures || size <= 0 || depth <= 0) {
-    fail(ECGPU_ERR_ARG, "ecgpu_pipeline_create_decode: bad arguments");
-    return nullptr;
-  }
-  const size_t n = size_t(k + m);
-  std::vector<int> out(n), src(n), coef(n * n);
-  int n_out = 0, n_src = 0;
-  if (ecgpu_decode_plan(k, m, w, matrix, row_k_ones, erasures, out.data(), &n_out, src.data(), &n_src,
-                        coef.data()) != ECGPU_OK) {
-    fail(ECGPU_ERR, "ecgpu_pipeline_create_decode: erasure pattern not decodable (reference decode returns -1)");
-    return nullptr;
-  }
-  return pipeline_build(k, m, n_out, n_src, coef.data(), src.data(), out.data(), size, depth, device);
-}
-
-
-namespace {
-bool pipe_d2h_worker_enabled() {
-  static const bool v = env_int("ECGPU_PIPE_D2H_WORKER", 1) != 0;
-  return v;
-}
-
-// D2H of a slot's outputs to the host pointers hp (s_d2h, after the slot's
-// compute), then the slot's drained event.
-int pipeline_d2h(ecgpu_pipeline* p, int sl, const std::vector<char*>& hp) {
-  ECGPU_HIP(hipStreamWaitEvent(p->s_d2h, p->computed[sl], 0));
-  if (int rc = copy_shards(false, p->slot_shard(sl, p->nsrc()), p->slot_stride, hp, size_t(p->size), p->s_d2h))
-    return rc;
-  ECGPU_HIP(hipEventRecord(p->drained[sl], p->s_d2h));
-  return ECGPU_OK;
-}
-
-void pipeline_d2h_worker(ecgpu_pipeline* p) {
-  (void)hipSetDevice(p->device);  // once: this thread only ever drives this device
-  for (;;) {
-    ecgpu_pipeline::D2HJob job;
-    {
-      std::unique_lock<std::mutex> lk(p->qmu);
-      p->qcv.wait(lk, [&] { return p->stop || !p->q.empty(); });
-      if (p->q.empty()) return;  // stop, nothing left
-      job = std::move(p->q.front());
-      p->q.pop_front();
-    }
-    int rc = ECGPU_OK;
-    bool failed_before = false;
-    {
-      std::lock_guard<std::mutex> lk(p->qmu);
-      failed_before = p->worker_rc != ECGPU_OK;
-    }
-    if (!failed_before) rc = pipeline_d2h(p, job.slot, job.hp);
-    std::lock_guard<std::mutex> lk(p->qmu);
-    if (rc != ECGPU_OK && p->worker_rc == ECGPU_OK) {
-      p->worker_rc = rc;
-      p->worker_err = t_err;
-    }
-    p->issued_below = job.ticket + 1;
-    p->qcv.notify_all();
-  }
-}
-
-// Queues stripe t into ring slot t % depth: H2D of the sources (s_h2d), the
-// fused apply (s_comp), then D2H of the outputs (s_d2h) -- issued here, or
-// by the pipeline's D2H worker when an output is pageable.
-int pipeline_enqueue(ecgpu_pipeline* p, int sl, int64_t t, char** data_ptrs, char** coding_ptrs) {
-  auto host = [&](int id) { return id < p->k ? data_ptrs[id] : coding_ptrs[id - p->k]; };
-  const int ns = p->nsrc(), nr = p->rows();
-  const size_t bytes = size_t(p->size);
-  std::vector<char*> hp;
-  int rc = ECGPU_OK;
-  if (nr > 0) {  // nothing to read when no shard is written
-    for (int j = 0; j < ns; ++j) hp.push_back(host(p->src_ids[j]));
-    if ((rc = copy_shards(true, p->slot_shard(sl, 0), p->slot_stride, hp, bytes, p->s_h2d)) != ECGPU_OK) return rc;
-  }
-  ECGPU_HIP(hipEventRecord(p->loaded[sl], p->s_h2d));
-  ECGPU_HIP(hipStreamWaitEvent(p->s_comp, p->loaded[sl], 0));
-  if (ns > 0 && nr > 0) {
-    if ((rc = plan_launch(p->plans[sl], p->s_comp)) != ECGPU_OK) return rc;
-  } else {
-    for (int i = 0; i < nr; ++i)  // rows with no source: all-zero output
-      ECGPU_HIP(hipMemsetAsync(p->slot_shard(sl, ns + i), 0, bytes, p->s_comp));
-  }
-  ECGPU_HIP(hipEventRecord(p->computed[sl], p->s_comp));
-  hp.clear();
-  for (int i = 0; i < nr; ++i) hp.push_back(host(p->out_ids[i]));
-  bool pageable = false;
-  for (char* h : hp) pageable = pageable || !is_pinned(h);
-  std::unique_lock<std::mutex> lk(p->qmu);
-  if (p->worker_rc != ECGPU_OK) return fail(p->worker_rc, p->worker_err);
-  if ((pageable && pipe_d2h_worker_enabled()) || !p->q.empty()) {
-    // behind any pending job, so s_d2h keeps submission order
-    if (!p->worker.joinable()) p->worker = std::thread(pipeline_d2h_worker, p);
-    p->q.push_back(ecgpu_pipeline::D2HJob{sl, t, std::move(hp)});
-    lk.unlock();
-    p->qcv.notify_all();
-    return ECGPU_OK;
-  }
-  lk.unlock();
-  if ((rc = pipeline_d2h(p, sl, hp)) != ECGPU_OK) return rc;
-  lk.lock();
-  p->issued_below = t + 1;
-  return ECGPU_OK;
-}
-}  // namespace
-
-ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, char** coding_ptrs) {
-  if (!p || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_submit: bad arguments");
-  std::lock_guard<std::mutex> lk(p->mu);
-  DeviceGuard g(p->device);
-  const int64_t t = p->next_ticket;
-  const int sl = int(t % p->depth);
-  int rc = pipeline_retire(p, sl);  // the slot's previous stripe must be out
-  if (rc != ECGPU_OK) return rc;
-  rc = pipeline_enqueue(p, sl, t, data_ptrs, coding_ptrs);
-  if (rc != ECGPU_OK) {
-    // part of the stripe may already be queued against the caller's buffers:
-    // let it finish before reporting, so no DMA outlives the failed call
-    const std::string msg = t_err;
-    for (hipStream_t s : {p->s_h2d, p->s_comp, p->s_d2h}) (void)hipStreamSynchronize(s);
-    t_err = msg;
-    return rc;
-  }
-  p->slot_ticket[sl] = t;
-  p->next_ticket = t + 1;
-  return t;
-}
-
-ECGPU_API int ecgpu_pipeline_wait(ecgpu_pipeline* p, int64_t ticket) {
-  if (!p || ticket < 0) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_wait: bad arguments");
-  std::lock_guard<std::mutex> lk(p->mu);
-  if (ticket < p->done_below) return ECGPU_OK;
-  if (ticket >= p->next_ticket) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_wait: ticket not submitted");
-  // (event waits need no current-device switch)
-  // retire every slot up to and including the ticket's (completion is in order)
-  for (int64_t t = p->done_below; t <= ticket; ++t) {
-    const int rc = pipeline_retire(p, int(t % p->depth));
-    if (rc != ECGPU_OK) return rc;
-  }
-  return ECGPU_OK;
-}
-
-ECGPU_API int ecgpu_pipeline_drain(ecgpu_pipeline* p) {
-  if (!p) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_drain: null");
-  if (p->next_ticket == 0) return ECGPU_OK;
-  return ecgpu_pipeline_wait(p, p->next_ticket - 1);
-}
-
-ECGPU_API void ecgpu_pipeline_destroy(ecgpu_pipeline* p) {
-  if (!p) return;
-  (void)ecgpu_pipeline_drain(p);
-  pipeline_free(p);
-}
-
-// ---------------------------------------------- multi-device pipeline ----
-// Stripes are independent, so a process driving several GPUs
-// shards them round-robin: stripe t runs on member t % n as that member's
-// local ticket t / n.  No collective and no cross-device traffic.  Each
-// member is a complete single-device pipeline with its own ring and streams
-// AND its own submit thread, bound to its device once (hipSetDevice at
-// thread start, never again): group_submit only hands the stripe's pointer
-// lists to member t % n's queue (a per-member lock; tickets come from an
-// atomic counter, no group-wide lock) and returns, the worker issues the
-// stripe's copies and launch, so pageable staging on one device never holds
-// up another.  Waits sync on the member's events (no device switch).
-namespace {
-struct GroupJob {
-  std::vector<char*> data, coding;
-};
-
-struct GroupMember {
-  ecgpu_pipeline* p = nullptr;
-  int k = 0, m = 0, cap = 1;
-  std::thread worker;
-  std::mutex mu;
-  std::condition_variable cv_job, cv_done, cv_space;
-  std::map<int64_t, GroupJob> pending;  // local ticket -> job, handed in possibly out of order
-  int64_t next_local = 0;               // next local ticket the worker submits
-  int64_t failed_from = -1;             // first local ticket whose submit failed (sticky)
-  int failed_rc = ECGPU_OK;
-  std::string failed_msg;
-  bool stop = false;
-
-  void run() {
-    (void)hipSetDevice(p->device);  // once: every submit below runs on this device
-    std::unique_lock<std::mutex> lk(mu);
-    for (;;) {
-      cv_job.wait(lk, [&] { return stop || pending.count(next_local) != 0; });
-      auto it = pending.find(next_local);
-      if (it == pending.end()) return;  // stop, queue drained
-      GroupJob job = std::move(it->second);
-      pending.erase(it);
-      cv_space.notify_all();
-      int64_t r = 0;
-      if (failed_from < 0) {
-        lk.unlock();
-        r = ecgpu_pipeline_submit(p, job.data.data(), job.coding.data());
-        const std::string msg = r < 0 ? t_err : std::string();
-        lk.lock();
-        if (r < 0) {
-          failed_from = next_local;
-          failed_rc = int(r);
-          failed_msg = msg;
-        }
-      }
-      ++next_local;
-      cv_done.notify_all();
-    }
-  }
-};
-}  // namespace
-
-struct ecgpu_pipeline_group {
-  std::vector<std::unique_ptr<GroupMember>> members;
-  std::atomic<int64_t> next_ticket{0};
-};
-
-namespace {
-void group_free(ecgpu_pipeline_group* g) {
-  if (!g) return;
-  for (auto& mb : g->members) {
-    if (mb->worker.joinable()) {
-      {
-        std::lock_guard<std::mutex> lk(mb->mu);
-        mb->stop = true;
-      }
-      mb->cv_job.notify_all();
-      mb->worker.join();
-    }
-    ecgpu_pipeline_destroy(mb->p);
-  }
-  delete g;
-}
-
-ecgpu_pipeline_group* group_build(int ndev, const int* devices, int k, int m, int depth,
-                                  const std::function<ecgpu_pipeline*(int)>& make) {
-  if (ndev <= 0 || !devices) {
-    fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group: ndev > 0 and a device list required");
-    return nullptr;
-  }
-  auto* g = new ecgpu_pipeline_group();
-  for (int i = 0; i < ndev; ++i) {
-    ecgpu_pipeline* p = make(devices[i]);
-    if (!p) {  // make() left the message in ecgpu_last_error
-      const std::string msg = t_err;
-      group_free(g);
-      t_err = msg;
-      return nullptr;
-    }
-    auto mb = std::make_unique<GroupMember>();
-    mb->p = p;
-    mb->k = k;
-    mb->m = m;
-    mb->cap = std::max(1, depth);
-    g->members.push_back(std::move(mb));
-  }
-  for (auto& mb : g->members) {
-    GroupMember* raw = mb.get();
-    raw->worker = std::thread([raw] { raw->run(); });
-  }
-  return g;
-}
-}  // namespace
-
-ECGPU_API ecgpu_pipeline_group* ecgpu_pipeline_group_create(int k, int m, const int* matrix, int64_t size, int depth,
-                                                            int ndev, const int* devices) {
-  return group_build(ndev, devices, k, m, depth,
-                     [&](int dev) { return ecgpu_pipeline_create(k, m, matrix, size, depth, dev); });
-}
-
-ECGPU_API ecgpu_pipeline_group* ecgpu_pipeline_group_create_decode(int k, int m, int w, const int* matrix,
-                                                                   int row_k_ones, const int* erasures, int64_t size,
-                                                                   int depth, int ndev, const int* devices) {
-  return group_build(ndev, devices, k, m, depth, [&](int dev) {
-    return ecgpu_pipeline_create_decode(k, m, w, matrix, row_k_ones, erasures, size, depth, dev);
-  });
-}
-
-ECGPU_API int64_t ecgpu_pipeline_group_submit(ecgpu_pipeline_group* g, char** data_ptrs, char** coding_ptrs) {
-  if (!g || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_submit: bad arguments");
-  const int64_t n = int64_t(g->members.size());
-  const int64_t t = g->next_ticket.fetch_add(1);
-  GroupMember& mb = *g->members[size_t(t % n)];
-  GroupJob job;
-  job.data.assign(data_ptrs, data_ptrs + mb.k);
-  job.coding.assign(coding_ptrs, coding_ptrs + mb.m);
-  {
-    std::unique_lock<std::mutex> lk(mb.mu);
-    // back-pressure: at most `depth` stripes queued ahead of the worker
-    mb.cv_space.wait(lk, [&] { return int64_t(mb.pending.size()) < mb.cap || t / n <= mb.next_local; });
-    mb.pending.emplace(t / n, std::move(job));
-  }
-  mb.cv_job.notify_one();
-  return t;
-}
-
-ECGPU_API int ecgpu_pipeline_group_wait(ecgpu_pipeline_group* g, int64_t ticket) {
-  if (!g || ticket < 0) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_wait: bad arguments");
-  if (ticket >= g->next_ticket.load()) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_wait: ticket not submitted");
-  const int64_t n = int64_t(g->members.size());
-  GroupMember& mb = *g->members[size_t(ticket % n)];
-  const int64_t local = ticket / n;
-  {
-    std::unique_lock<std::mutex> lk(mb.mu);
-    mb.cv_done.wait(lk, [&] { return mb.next_local > local; });  // the worker has queued it
-    if (mb.failed_from >= 0 && local >= mb.failed_from) return fail(mb.failed_rc, mb.failed_msg);
-  }
-  return ecgpu_pipeline_wait(mb.p, local);
-}
-
-ECGPU_API int ecgpu_pipeline_group_drain(ecgpu_pipeline_group* g) {
-  if (!g) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_drain: null");
-  const int64_t end = g->next_ticket.load(), n = int64_t(g->members.size());
-  int rc = ECGPU_OK;
-  for (int64_t t = std::max<int64_t>(0, end - n); t < end; ++t) {  // each member's last ticket
-    const int r = ecgpu_pipeline_group_wait(g, t);
-    if (r != ECGPU_OK && rc == ECGPU_OK) rc = r;
-  }
-  return rc;
-}
-
-ECGPU_API int ecgpu_pipeline_group_size(ecgpu_pipeline_group* g) { return g ? int(g->members.size()) : 0; }
-
-ECGPU_API void ecgpu_pipeline_group_destroy(ecgpu_pipeline_group* g) {
-  if (!g) return;
-  (void)ecgpu_pipeline_group_drain(g);
-  group_free(g);
-}
 
 ECGPU_API int ecgpu_host_register(void* ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return fail(ECGPU_ERR_ARG, "ecgpu_host_register: bad arguments");
@@ -1927,341 +1213,6 @@ ECGPU_API int ecgpu_reed_sol_r6_encode(int k, int w, char** data_ptrs, char** co
   }
   const int rc = execute(t.finish(), size);
   return rc == ECGPU_OK ? 1 : rc;
-}
-
-}  // extern "C"
-
-// ------------------------------------------- GF(2) packet coding ----
-// Bit-matrix / schedule coding (jerasure.cpp:301-345, :623-703, :1153-1192,
-// :1346-1363).  The reference's memcpy / XOR sequence over packet rows is
-// replayed by the LinearTracker on virtual buffers "packet row r of device
-// slot s" (one super-packet), and the fused map runs once over every
-// super-packet (gf_xor_packets).
-namespace {
-
-inline int pslot(const void* k) { return PacketTracker::key_slot(k); }
-inline int prow(const void* k) { return PacketTracker::key_row(k); }
-constexpr int kMaxPacketRow = (1 << 20) - 1;
-
-constexpr int kPacketRows = 32;  // output packet rows per launch (uint32 masks)
-
-// Slot s's packet row r of super-packet sp is ptrs[s] + sp * spstride + r * ps.
-int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride, int64_t ps) {
-  add_stats(op);
-  if (op.dsts.empty() || nsp <= 0 || ps <= 0) return ECGPU_OK;
-  const int device = current_device();
-  CtxLease lease(device);
-  if (!lease.c) return lease.rc;
-  Ctx* c = lease.c;
-  DeviceGuard g(device);
-
-  // Slots touched and their byte extents.
-  std::vector<int> slots;
-  std::vector<int64_t> maxrow(ptrs.size(), -1);
-  std::vector<char> is_out(ptrs.size(), 0);
-  auto touch = [&](const void* key, bool out) -> int {
-    const int sl = pslot(key), r = prow(key);
-    if (sl < 0 || size_t(sl) >= ptrs.size() || !ptrs[size_t(sl)])
-      return fail(ECGPU_ERR_ARG, "packet op references a missing device pointer");
-    if (maxrow[size_t(sl)] < 0) slots.push_back(sl);
-    maxrow[size_t(sl)] = std::max<int64_t>(maxrow[size_t(sl)], r);
-    if (out) is_out[size_t(sl)] = 1;
-    return ECGPU_OK;
-  };
-  for (void* k : op.srcs)
-    if (int rc = touch(k, false)) return rc;
-  for (void* k : op.dsts)
-    if (int rc = touch(k, true)) return rc;
-  const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
-  const bool via_temp = op.dst_is_src && rows > kPacketRows;
-  const int ngroups = (rows + kPacketRows - 1) / kPacketRows;
-
-  // Staging slab: staged slots, temporaries, then the pointer / mask tables.
-  std::vector<uint8_t*> base(ptrs.size(), nullptr);
-  std::vector<char> staged(ptrs.size(), 0);
-  std::vector<int64_t> extent(ptrs.size(), 0);
-  size_t off = 0;
-  for (int sl : slots) {
-    extent[size_t(sl)] = (nsp - 1) * spstride + (maxrow[size_t(sl)] + 1) * ps;
-    bool on_dev = false;
-    if (int rc = classify(ptrs[size_t(sl)], device, &on_dev)) return rc;
-    if (on_dev) {
-      base[size_t(sl)] = reinterpret_cast<uint8_t*>(ptrs[size_t(sl)]);
-    } else {
-      staged[size_t(sl)] = 1;
-      base[size_t(sl)] = reinterpret_cast<uint8_t*>(off);  // offset, rebased below
-      off += (size_t(extent[size_t(sl)]) + 255) & ~size_t(255);
-    }
-  }
-  const size_t temp_off = off;
-  if (via_temp) off += size_t(rows) * size_t(nsp * ps + 255 & ~int64_t(255));
-  const size_t tab_off = off;
-  const size_t tab_bytes = sizeof(void*) * size_t(nsrc + rows) + sizeof(uint32_t) * size_t(nsrc) * ngroups;
-  off += tab_bytes;
-  if (int rc = ensure_stage(c, off)) return rc;
-  for (int sl : slots)
-    if (staged[size_t(sl)]) {
-      base[size_t(sl)] = c->stage + reinterpret_cast<size_t>(base[size_t(sl)]);
-      // outputs too: packets the op does not write must come back unchanged
-      ECGPU_HIP(hipMemcpyAsync(base[size_t(sl)], ptrs[size_t(sl)], size_t(extent[size_t(sl)]),
-                               hipMemcpyHostToDevice, c->stream));
-    }
-
-  std::vector<const uint8_t*> sb(static_cast<size_t>(nsrc));
-  std::vector<uint8_t*> db(static_cast<size_t>(rows));
-  const int64_t temp_stride = (nsp * ps + 255) & ~int64_t(255);
-  for (int j = 0; j < nsrc; ++j) sb[size_t(j)] = base[size_t(pslot(op.srcs[size_t(j)]))] + prow(op.srcs[size_t(j)]) * ps;
-  for (int r = 0; r < rows; ++r)
-    db[size_t(r)] = via_temp ? c->stage + temp_off + size_t(r) * size_t(temp_stride)
-                             : base[size_t(pslot(op.dsts[size_t(r)]))] + prow(op.dsts[size_t(r)]) * ps;
-  std::vector<uint32_t> masks(size_t(nsrc) * ngroups, 0u);
-  for (int r = 0; r < rows; ++r)
-    for (int j = 0; j < nsrc; ++j)
-      if (op.coef[size_t(r) * nsrc + j]) masks[size_t(r / kPacketRows) * nsrc + j] |= 1u << (r % kPacketRows);
-  // one upload of [src bases | dst bases | masks]
-  std::vector<uint8_t> host_tab(tab_bytes);
-  std::memcpy(host_tab.data(), sb.data(), sizeof(void*) * nsrc);
-  std::memcpy(host_tab.data() + sizeof(void*) * nsrc, db.data(), sizeof(void*) * rows);
-  std::memcpy(host_tab.data() + sizeof(void*) * size_t(nsrc + rows), masks.data(), masks.size() * sizeof(uint32_t));
-  uint8_t* tab = c->stage + tab_off;
-  auto* d_src = reinterpret_cast<const uint8_t**>(tab);
-  auto* d_dst = reinterpret_cast<uint8_t**>(tab + sizeof(void*) * nsrc);
-  auto* d_mask = reinterpret_cast<uint32_t*>(tab + sizeof(void*) * size_t(nsrc + rows));
-  ECGPU_HIP(hipMemcpyAsync(tab, host_tab.data(), tab_bytes, hipMemcpyHostToDevice, c->stream));
-
-  const int64_t dstride = via_temp ? ps : spstride;
-  bool aligned = ps % 8 == 0 && spstride % 8 == 0 && dstride % 8 == 0;
-  for (auto* p : sb) aligned &= (reinterpret_cast<uintptr_t>(p) & 7u) == 0;
-  for (auto* p : db) aligned &= (reinterpret_cast<uintptr_t>(p) & 7u) == 0;
-  // 16-B lanes when everything is 16-B aligned; ECGPU_PACKET=1 forces 8-B
-  // lanes, 2 the unpipelined 16-B kernel (A/B, RS(10,4) w = 8 64 MiB
-  // bit-matrix encode on MI355X: pipelined 16-B lanes 180.5 us, unpipelined
-  // with 8 rows in flight 187, 8-B lanes 190; profiles/r02_packet_ab.txt)
-  const int packet_kind = env_int("ECGPU_PACKET", 0);
-  bool wide16 = aligned && packet_kind != 1 && ps % 16 == 0 && spstride % 16 == 0 && dstride % 16 == 0;
-  for (auto* p : sb) wide16 &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
-  for (auto* p : db) wide16 &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
-  for (int g0 = 0; g0 < ngroups; ++g0) {
-    const int R = std::min(kPacketRows, rows - g0 * kPacketRows);
-    dev::PacketArgs a{};
-    a.src = d_src;
-    a.dst = d_dst + size_t(g0) * kPacketRows;
-    a.mask = d_mask + size_t(g0) * nsrc;
-    a.sstride = spstride;
-    a.dstride = dstride;
-    a.nsrc = nsrc;
-    a.R = R;
-    a.cpp = wide16 ? ps / 16 : aligned ? ps / 8 : ps;
-    a.ncols = nsp * a.cpp;
-    if (nsrc == 0) {  // every output packet is zero
-      for (int r = 0; r < R; ++r)
-        ECGPU_HIP(hipMemset2DAsync(db[size_t(g0 * kPacketRows + r)], size_t(nsp > 1 ? dstride : ps), 0, size_t(ps),
-                                   size_t(nsp), c->stream));
-      continue;
-    }
-    void* fn = nullptr;
-    if (wide16 && packet_kind == 2)
-      fn = R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets16<8, 8>)
-           : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets16<16, 8>)
-                     : reinterpret_cast<void*>(&dev::gf_xor_packets16<32, 8>);
-    else if (wide16)
-      fn = R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets16p<8>)
-           : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets16p<16>)
-                     : reinterpret_cast<void*>(&dev::gf_xor_packets16p<32>);
-    else
-      fn = aligned ? (R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets<8>)
-                      : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets<16>)
-                                : reinterpret_cast<void*>(&dev::gf_xor_packets<32>))
-                   : reinterpret_cast<void*>(&dev::gf_xor_packets_bytes);
-    void* args[] = {&a};
-    const dim3 grid(unsigned((a.ncols + dev::kBlock - 1) / dev::kBlock));
-    ECGPU_HIP(hipLaunchKernel(fn, grid, dim3(dev::kBlock), args, 0, c->stream));
-  }
-  if (via_temp)
-    for (int r = 0; r < rows; ++r) {
-      uint8_t* real = base[size_t(pslot(op.dsts[size_t(r)]))] + prow(op.dsts[size_t(r)]) * ps;
-      ECGPU_HIP(hipMemcpy2DAsync(real, size_t(nsp > 1 ? spstride : ps), db[size_t(r)], size_t(ps), size_t(ps),
-                                 size_t(nsp), hipMemcpyDeviceToDevice, c->stream));
-    }
-  for (int sl : slots)
-    if (staged[size_t(sl)] && is_out[size_t(sl)])
-      ECGPU_HIP(hipMemcpyAsync(ptrs[size_t(sl)], base[size_t(sl)], size_t(extent[size_t(sl)]), hipMemcpyDeviceToHost,
-                               c->stream));
-  ECGPU_HIP(hipStreamSynchronize(c->stream));
-  ECGPU_HIP(hipGetLastError());
-  return ECGPU_OK;
-}
-
-// jerasure_bitmatrix_dotprod (jerasure.cpp:301-345) for ONE super-packet on
-// virtual packet rows; byte counters scaled by the super-packet count.
-void record_bitmatrix_dotprod(PacketTracker& t, int k, int w, const int* row, const int* src_ids, int dest_id,
-                              int64_t ps, int64_t nsp) {
-  int index = 0;
-  for (int j = 0; j < w; ++j) {
-    bool started = false;
-    for (int x = 0; x < k; ++x) {
-      const int dev = src_ids ? src_ids[x] : x;
-      for (int y = 0; y < w; ++y, ++index) {
-        if (!row[index]) continue;
-        if (!started) {
-          t.copy(dest_id, j, dev, y);
-          t.count(0, 0, double(ps) * double(nsp));
-          started = true;
-        } else {
-          t.xor_into(dest_id, j, dev, y);
-          t.count(double(ps) * double(nsp), 0, 0);
-        }
-      }
-    }
-  }
-}
-
-std::vector<char*> device_ptrs(int k, int n, char** data, char** coding) {
-  std::vector<char*> p(static_cast<size_t>(n), nullptr);
-  for (int i = 0; i < n; ++i) p[size_t(i)] = i < k ? data[i] : coding[i - k];
-  return p;
-}
-
-// Devices and packet rows a schedule names (ops[i] = {src dev, src packet,
-// dst dev, dst packet, xor?}, terminated by ops[i][0] < 0).
-int schedule_extent(int** ops, int* max_dev, int* max_row) {
-  *max_dev = -1;
-  *max_row = -1;
-  for (int i = 0; ops[i][0] >= 0; ++i) {
-    const int* o = ops[i];
-    if (o[1] < 0 || o[3] < 0 || o[1] > kMaxPacketRow || o[3] > kMaxPacketRow || o[2] < 0)
-      return fail(ECGPU_ERR_ARG, "schedule op out of range");
-    *max_dev = std::max(*max_dev, std::max(o[0], o[2]));
-    *max_row = std::max(*max_row, std::max(o[1], o[3]));
-  }
-  return ECGPU_OK;
-}
-
-// Replays a schedule for one super-packet.
-void record_schedule(PacketTracker& t, int** ops, int64_t ps, int64_t nsp) {
-  for (int i = 0; ops[i][0] >= 0; ++i) {
-    const int* o = ops[i];
-    if (o[4]) {
-      t.xor_into(o[2], o[3], o[0], o[1]);
-      t.count(double(ps) * double(nsp), 0, 0);
-    } else {
-      t.copy(o[2], o[3], o[0], o[1]);
-      t.count(0, 0, double(ps) * double(nsp));
-    }
-  }
-}
-
-}  // namespace
-
-extern "C" {
-
-ECGPU_API int ecgpu_jerasure_bitmatrix_dotprod(int k, int w, int* bitmatrix_row, int* src_ids, int dest_id,
-                                               char** data_ptrs, char** coding_ptrs, int size, int packetsize) {
-  if (k <= 0 || w <= 0 || packetsize <= 0 || !bitmatrix_row || size % (w * packetsize) != 0)
-    return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_bitmatrix_dotprod: size % (w*packetsize) must be 0");
-  const int64_t nsp = size / (int64_t(w) * packetsize);
-  int n = std::max(k, dest_id + 1);
-  if (src_ids)
-    for (int x = 0; x < k; ++x) n = std::max(n, src_ids[x] + 1);
-  PacketTracker t(n, w);
-  record_bitmatrix_dotprod(t, k, w, bitmatrix_row, src_ids, dest_id, packetsize, nsp);
-  // ids >= k index coding_ptrs; only the ids the op touches are dereferenced
-  std::vector<char*> p(static_cast<size_t>(n), nullptr);
-  auto put = [&](int id) { p[size_t(id)] = id < k ? data_ptrs[id] : coding_ptrs[id - k]; };
-  put(dest_id);
-  for (int x = 0; x < k; ++x) put(src_ids ? src_ids[x] : x);
-  return execute_packets(t.finish(), p, nsp, int64_t(w) * packetsize, packetsize);
-}
-
-ECGPU_API int ecgpu_jerasure_bitmatrix_encode(int k, int m, int w, int* bitmatrix, char** data_ptrs,
-                                              char** coding_ptrs, int size, int packetsize) {
-  if (k <= 0 || m <= 0 || w <= 0 || packetsize <= 0 || !bitmatrix || size % (w * packetsize) != 0)
-    return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_bitmatrix_encode: size % (packetsize*w) must be 0");
-  const int64_t nsp = size / (int64_t(w) * packetsize);
-  PacketTracker t(k + m, w);
-  for (int i = 0; i < m; ++i)
-    record_bitmatrix_dotprod(t, k, w, bitmatrix + size_t(i) * k * w * w, nullptr, k + i, packetsize, nsp);
-  return execute_packets(t.finish(), device_ptrs(k, k + m, data_ptrs, coding_ptrs), nsp, int64_t(w) * packetsize,
-                         packetsize);
-}
-
-// jerasure.cpp:623-703 as one fused GF(2) map.
-ECGPU_API int ecgpu_jerasure_bitmatrix_decode(int k, int m, int w, int* bitmatrix, int row_k_ones, int* erasures,
-                                              char** data_ptrs, char** coding_ptrs, int size, int packetsize) {
-  if (k <= 0 || m <= 0 || w <= 0 || packetsize <= 0 || !bitmatrix || !erasures || size % (w * packetsize) != 0)
-    return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_bitmatrix_decode: bad arguments");
-  int* erased = erasures_to_erased(k, m, erasures);
-  if (!erased) return ECGPU_ERR;
-  const int64_t nsp = size / (int64_t(w) * packetsize);
-  int edd = 0, lastdrive = k;
-  for (int i = 0; i < k; ++i)
-    if (erased[i]) {
-      ++edd;
-      lastdrive = i;
-    }
-  if (row_k_ones != 1 || erased[k]) lastdrive = k;
-  const size_t blk = size_t(k) * w * w;
-  std::vector<int> dm, ids;
-  if (edd > 1 || (edd > 0 && (row_k_ones != 1 || erased[k]))) {
-    dm.resize(blk * k);
-    ids.resize(size_t(k));
-    if (make_decoding_bitmatrix(k, m, w, bitmatrix, erased, dm.data(), ids.data()) < 0) {
-      std::free(erased);
-      return ECGPU_ERR;
-    }
-  }
-  PacketTracker t(k + m, w);
-  for (int i = 0; edd > 0 && i < lastdrive; ++i)
-    if (erased[i]) {
-      record_bitmatrix_dotprod(t, k, w, dm.data() + i * blk, ids.data(), i, packetsize, nsp);
-      --edd;
-    }
-  if (edd > 0) {
-    std::vector<int> tmp(static_cast<size_t>(k));
-    for (int i = 0; i < k; ++i) tmp[size_t(i)] = i < lastdrive ? i : i + 1;
-    record_bitmatrix_dotprod(t, k, w, bitmatrix, tmp.data(), lastdrive, packetsize, nsp);
-  }
-  for (int i = 0; i < m; ++i)
-    if (erased[k + i]) record_bitmatrix_dotprod(t, k, w, bitmatrix + i * blk, nullptr, k + i, packetsize, nsp);
-  std::free(erased);
-  return execute_packets(t.finish(), device_ptrs(k, k + m, data_ptrs, coding_ptrs), nsp, int64_t(w) * packetsize,
-                         packetsize);
-}
-
-// jerasure.cpp:1153-1176: one super-packet at ptrs.
-ECGPU_API int ecgpu_jerasure_do_scheduled_operations(char** ptrs, int** operations, int packetsize) {
-  if (!ptrs || !operations || packetsize <= 0)
-    return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_do_scheduled_operations: bad arguments");
-  int max_dev = -1, max_row = -1;
-  if (int rc = schedule_extent(operations, &max_dev, &max_row)) return rc;
-  if (max_dev < 0) return ECGPU_OK;
-  PacketTracker t(max_dev + 1, max_row + 1);
-  record_schedule(t, operations, packetsize, 1);
-  std::vector<char*> p(ptrs, ptrs + (max_dev + 1));
-  return execute_packets(t.finish(), p, 1, 0, packetsize);
-}
-
-// jerasure.cpp:1178-1192 over nptrs device pointers (NULL where unused), and
-// the decode-time schedules of jerasure.cpp:935-995.
-ECGPU_API int ecgpu_schedule_run(int nptrs, char** ptrs, int** operations, int w, int size, int packetsize) {
-  if (nptrs <= 0 || !ptrs || !operations || w <= 0 || packetsize <= 0 || size % (w * packetsize) != 0)
-    return fail(ECGPU_ERR_ARG, "ecgpu_schedule_run: size % (w*packetsize) must be 0");
-  const int64_t nsp = size / (int64_t(w) * packetsize);
-  int max_dev = -1, max_row = -1;
-  if (int rc = schedule_extent(operations, &max_dev, &max_row)) return rc;
-  if (max_dev >= nptrs) return fail(ECGPU_ERR_ARG, "ecgpu_schedule_run: schedule names a device >= nptrs");
-  if (max_dev < 0) return ECGPU_OK;
-  PacketTracker t(max_dev + 1, max_row + 1);
-  record_schedule(t, operations, packetsize, nsp);
-  std::vector<char*> p(ptrs, ptrs + nptrs);
-  return execute_packets(t.finish(), p, nsp, int64_t(w) * packetsize, packetsize);
-}
-
-ECGPU_API int ecgpu_jerasure_schedule_encode(int k, int m, int w, int** schedule, char** data_ptrs, char** coding_ptrs,
-                                             int size, int packetsize) {
-  if (k <= 0 || m <= 0) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_schedule_encode: bad arguments");
-  std::vector<char*> p = device_ptrs(k, k + m, data_ptrs, coding_ptrs);
-  return ecgpu_schedule_run(k + m, p.data(), schedule, w, size, packetsize);
 }
 
 ECGPU_API int ecgpu_jerasure_get_stats(double* fill_in) {

@@ -1,0 +1,142 @@
+// runtime.hpp -- internal interface shared by the runtime's translation
+// units (not installed; the public surface is include/ecgpu.h):
+//   ecgpu_runtime.hip  plans, kernel dispatch, contexts, staging of host
+//                      buffers, synchronous calls and their C ABI
+//   accum.hip          HBM-resident ECX parity accumulators
+//   pipeline.hip       host-memory pipelines and multi-device groups
+//   packets.hip        GF(2) bit-matrix / schedule coding
+// Everything here lives in ecgpu::rt with hidden visibility: the shared
+// library exports only the ECGPU_API functions.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <list>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "ecgpu.h"
+#include "gf_kernels.hpp"
+#include "planner.hpp"
+
+#define ECGPU_RT_BEGIN \
+  namespace ecgpu {    \
+  namespace __attribute__((visibility("hidden"))) rt {
+#define ECGPU_RT_END \
+  }                  \
+  }
+
+// A bound coefficient matrix (ecgpu_plan_* in include/ecgpu.h).
+struct ecgpu_plan {
+  int device = 0, rows = 0, nsrc = 0, w = 8;
+  int kind = ECGPU_KERNEL_PERM, nt = 1;
+  std::vector<uint32_t> coef;  // host copy, rows x nsrc
+  // one device allocation for all coefficient tables, carved below
+  uint8_t* d_tabs = nullptr;
+  ecgpu::dev::u32x4* d_q = nullptr;
+  uint32_t* d_p3 = nullptr;    // 3-bit-slice tables, kP3Words per coefficient
+  uint8_t* d_nib = nullptr;
+  uint32_t* d_w = nullptr;     // wide-word tables (w = 16 / 32)
+  uint8_t* d_wcls = nullptr;   // wide coefficient classes
+  uint32_t* d_wnib = nullptr;  // wide-word LDS nibble tables, kNibWords per coefficient
+  int stripes = 0;
+  int64_t size = 0;
+  bool aligned = true;
+  // one device allocation for the pointer tables: sources, then destinations
+  void** d_ptrs = nullptr;
+  size_t cap_ptrs = 0;
+  const uint8_t** d_src = nullptr;
+  uint8_t** d_dst = nullptr;
+};
+
+ECGPU_RT_BEGIN
+
+// ---- errors and knobs -------------------------------------------------------
+extern thread_local std::string t_err;  // ecgpu_last_error()
+int fail(int code, const std::string& msg);
+int env_int(const char* name, int dflt);
+
+#define ECGPU_HIP(expr)                                                                          \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      return ::ecgpu::rt::fail(ECGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int current_device();
+
+// ---- plans --------------------------------------------------------------------
+void plan_free(ecgpu_plan* p);
+int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, int w = 8);
+// With a stream the pointer tables are uploaded asynchronously on it; unless
+// `keep_alive` (the caller keeps src/dst alive until it synchronises the
+// stream) the call waits for the upload.
+int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* const* dst, int64_t size,
+              hipStream_t stream, bool keep_alive = false);
+int plan_launch(ecgpu_plan* p, hipStream_t stream);
+
+// ---- contexts of the synchronous calls ----------------------------------------
+struct PlanKey {
+  int rows, nsrc, w;
+  std::vector<uint32_t> coef;
+  bool operator==(const PlanKey& o) const { return rows == o.rows && nsrc == o.nsrc && w == o.w && coef == o.coef; }
+};
+
+struct Ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* stage = nullptr;
+  size_t stage_cap = 0;
+  uint8_t* bounce = nullptr;  // pinned host mirror of the staging slab (mid-size calls, see execute)
+  size_t bounce_cap = 0;
+  uint8_t* zc = nullptr;      // coherent pinned memory the kernel reads / writes in place (small calls)
+  size_t zc_cap = 0;
+  std::list<std::pair<PlanKey, ecgpu_plan*>> plans;  // LRU, front = newest
+};
+
+Ctx* acquire_ctx(int device, int* rc);
+void release_ctx(Ctx* c);
+
+struct CtxLease {
+  int rc = ECGPU_OK;  // declared first: initialised before acquire_ctx writes it
+  Ctx* c = nullptr;
+  explicit CtxLease(int device) : c(acquire_ctx(device, &rc)) {}
+  ~CtxLease() {
+    if (c) release_ctx(c);
+  }
+};
+
+int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int w, ecgpu_plan** out);
+int ensure_bounce(Ctx* c, size_t bytes);
+int ensure_zc(Ctx* c, size_t bytes);
+int ensure_stage(Ctx* c, size_t bytes);
+
+// ---- host memory --------------------------------------------------------------
+bool zero_copy_pinned();
+int classify(const void* p, int device, bool* on_device);
+bool host_mapped(const void* p, size_t bytes, void** dev);
+bool is_pinned(const void* p);
+int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>& hp, size_t bytes, hipStream_t s);
+
+// ---- synchronous execution ----------------------------------------------------
+void add_stats(const FusedOp& op);
+bool inline_ok(const FusedOp& op);
+int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, const std::vector<uint8_t*>& dp,
+                  int64_t size, hipStream_t s, bool host_io);
+int execute(const FusedOp& op, int64_t size);
+
+ECGPU_RT_END

@@ -53,6 +53,12 @@ def test_c_abi_loads_and_exports_everything():
     for name in decl:
         getattr(lib, name)
     assert lib.ecgpu_version
+    # the runtime's internals (ecgpu::rt, kernel tables, anonymous helpers)
+    # stay hidden: only the C ABI is exported (weak libstdc++ instantiations
+    # are vague-linkage artefacts, not API)
+    std_prefixes = ("_ZNSt", "_ZNKSt", "_ZSt", "_ZZNSt", "_ZNK9__gnu_cxx", "_ZN9__gnu_cxx")
+    leaked = sorted(n for n in exported(path) if not n.startswith(("ecgpu_",) + std_prefixes))
+    assert not leaked, leaked[:20]
 
 
 def test_python_binding_covers_header():

@@ -703,13 +703,17 @@ def test_host_pipeline_decoder_rejects_undecodable(ec, gpu):
 # The one-GPU box repeats device 0 in the member list: the round-robin
 # ticket mapping, per-member rings and out-of-order waits are what is tested
 # here; members on distinct devices differ only in the device ordinal.
+@pytest.mark.parametrize("memory", ["pinned", "pageable"])  # pageable: every member's D2H worker
 @pytest.mark.parametrize("members", [1, 2, 3])
-def test_pipeline_group_encode_round_robin(ec, gpu, restatement, members):
+def test_pipeline_group_encode_round_robin(ec, gpu, restatement, members, memory):
     import torch
     k, m, size, stripes = 10, 4, (1 << 18) + 7, 8
     M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
-    data = [[torch.from_numpy(b).pin_memory() for b in host_shards(60, s, k, size)] for s in range(stripes)]
-    coding = [[torch.zeros(size + PAD, dtype=torch.uint8).pin_memory() for _ in range(m)] for _ in range(stripes)]
+    data = [[torch.from_numpy(b) for b in host_shards(60, s, k, size)] for s in range(stripes)]
+    coding = [[torch.zeros(size + PAD, dtype=torch.uint8) for _ in range(m)] for _ in range(stripes)]
+    if memory == "pinned":
+        data = [[b.pin_memory() for b in st] for st in data]
+        coding = [[b.pin_memory() for b in st] for st in coding]
     g = ec.HostPipelineGroup(k, m, M, size, devices=[0] * members, depth=2)
     assert ec._native.lib.ecgpu_pipeline_group_size(g._g) == members
     tickets = [g.submit(data[s], coding[s]) for s in range(stripes)]

@@ -130,6 +130,18 @@ int main() {
     std::free(fresh);
     std::free(used);
   }
+  // the H2D of one stripe split over two issuing threads (two streams)
+  hipStream_t s_in2;
+  CK(hipStreamCreateWithFlags(&s_in2, hipStreamNonBlocking));
+  bench("H2D 10 x 4 MiB from two threads (5 shards each)", [&] {
+    std::thread t([&] {
+      for (int j = 5; j < k; ++j) CK(hipMemcpyAsync(dev + j * S, hin[j], S, hipMemcpyHostToDevice, s_in2));
+      CK(hipStreamSynchronize(s_in2));
+    });
+    for (int j = 0; j < 5; ++j) CK(hipMemcpyAsync(dev + j * S, hin[j], S, hipMemcpyHostToDevice, s_in));
+    CK(hipStreamSynchronize(s_in));
+    t.join();
+  });
   bench("H2D 10 x 4 MiB alone", h2d);
   bench("D2H 4 x 4 MiB alone", d2h);
   bench("H2D then D2H, one thread", [&] {

@@ -467,7 +467,7 @@ def config_block(E, N, dev, stream, kind, nt, main=None):
     e["host_decode_plan_us"] = round(median(host_us), 2)
     e["host_plan_create_us"] = round(median(create_us), 2)
     e["host_note"] = ("host_decode_plan_us: ecgpu_decode_plan (survivor choice, k x k inversion, fused map) through "
-                      "ctypes; host_plan_create_us: the whole DecodePlan incl. coefficient tables and their upload; "
+                      "ctypes; host_plan_create_us: the whole DecodePlan incl. coefficient tables and their (asynchronous) upload; "
                       "medians, not in the launch time")
     out["C4_decode_0123"] = e
     dp.close()

@@ -214,9 +214,79 @@ ECGPU_RT_END
 ECGPU_RT_BEGIN
 
 
+// One non-blocking stream per device for coefficient-table uploads: a plan's
+// creation does not wait for its tables (one blocking copy cost ~12 us,
+// tools/hip_overheads.cpp); its launches wait on the upload's event instead.
+hipStream_t upload_stream(int device) {
+  static std::mutex mu;
+  static std::vector<hipStream_t> streams;
+  std::lock_guard<std::mutex> lk(mu);
+  if (size_t(device) >= streams.size()) streams.resize(size_t(device) + 1, nullptr);
+  if (!streams[size_t(device)]) {
+    DeviceGuard g(device);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    streams[size_t(device)] = s;
+  }
+  return streams[size_t(device)];
+}
+
+// Allocates p->d_tabs and uploads `host` into it without waiting (the plan
+// keeps `host` alive until the upload has completed).
+int plan_upload_tables(ecgpu_plan* p, std::vector<uint8_t>&& host) {
+  DeviceGuard g(p->device);
+  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_tabs), host.size()));
+  p->host_tabs = std::move(host);
+  const hipStream_t s = upload_stream(p->device);
+  if (!s) {  // no stream: a blocking copy
+    ECGPU_HIP(hipMemcpy(p->d_tabs, p->host_tabs.data(), p->host_tabs.size(), hipMemcpyHostToDevice));
+    return ECGPU_OK;
+  }
+  ECGPU_HIP(hipEventCreateWithFlags(&p->uploaded, hipEventDisableTiming));
+  ECGPU_HIP(hipMemcpyAsync(p->d_tabs, p->host_tabs.data(), p->host_tabs.size(), hipMemcpyHostToDevice, s));
+  ECGPU_HIP(hipEventRecord(p->uploaded, s));
+  p->upload_pending = true;
+  return ECGPU_OK;
+}
+
+// Waits for the plan's table upload on the host (a no-op once it completed).
+int plan_sync_tables(ecgpu_plan* p) {
+  if (!p->upload_pending) return ECGPU_OK;
+  ECGPU_HIP(hipEventSynchronize(p->uploaded));
+  p->upload_pending = false;
+  std::vector<uint8_t>().swap(p->host_tabs);
+  return ECGPU_OK;
+}
+
+// Orders `stream` after the plan's table upload (a no-op once it completed).
+// A blocking bind has already waited for it, so a bound plan launches inside
+// a stream capture without touching the event; a plan bound on a stream
+// (the synchronous calls) may not be captured before its upload completed.
+int plan_wait_tables(ecgpu_plan* p, hipStream_t stream) {
+  if (!p->upload_pending) return ECGPU_OK;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+    return fail(ECGPU_ERR, "plan tables still uploading: bind the plan without a stream before capturing it");
+  (void)hipGetLastError();
+  const hipError_t q = hipEventQuery(p->uploaded);
+  if (q == hipSuccess) {
+    p->upload_pending = false;
+    std::vector<uint8_t>().swap(p->host_tabs);
+    return ECGPU_OK;
+  }
+  if (q != hipErrorNotReady) return fail(ECGPU_ERR_HIP, std::string("table upload: ") + hipGetErrorString(q));
+  (void)hipGetLastError();  // not ready is not an error
+  ECGPU_HIP(hipStreamWaitEvent(stream, p->uploaded, 0));
+  return ECGPU_OK;
+}
+
 void plan_free(ecgpu_plan* p) {
   if (!p) return;
   DeviceGuard g(p->device);
+  if (p->uploaded) {
+    (void)hipEventSynchronize(p->uploaded);  // the table upload may still read host_tabs
+    (void)hipEventDestroy(p->uploaded);
+  }
   if (p->d_tabs) (void)hipFree(p->d_tabs);
   if (p->d_ptrs) (void)hipFree(p->d_ptrs);
   delete p;
@@ -249,9 +319,7 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
     std::memcpy(host.data(), t.data(), tb);
     std::memcpy(host.data() + tb, nib.data(), nb);
     std::memcpy(host.data() + tb + nb, cls.data(), n);
-    DeviceGuard g(device);
-    ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_tabs), host.size()));
-    ECGPU_HIP(hipMemcpy(p->d_tabs, host.data(), host.size(), hipMemcpyHostToDevice));
+    if (int rc = plan_upload_tables(p, std::move(host))) return rc;
     p->d_w = reinterpret_cast<uint32_t*>(p->d_tabs);
     p->d_wnib = reinterpret_cast<uint32_t*>(p->d_tabs + tb);
     p->d_wcls = p->d_tabs + tb + nb;
@@ -263,15 +331,14 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
   std::vector<uint8_t> nib(n * 32);
   for (size_t i = 0; i < n; ++i) build_tables(coefs[i], &q[i], &p3[i * dev::kP3Words], &nib[i * 32]);
   // [2-bit tables | 3-bit tables | nibble tables] in one allocation, ONE
-  // upload (three blocking copies cost ~12 us each, tools/hip_overheads.cpp)
+  // asynchronous upload (plan_upload_tables; three blocking copies cost ~12 us
+  // each, tools/hip_overheads.cpp)
   const size_t qb = n * sizeof(u32x4), pb = p3.size() * sizeof(uint32_t), nb = n * 32;
   std::vector<uint8_t> host(qb + pb + nb);
   std::memcpy(host.data(), q.data(), qb);
   std::memcpy(host.data() + qb, p3.data(), pb);
   std::memcpy(host.data() + qb + pb, nib.data(), nb);
-  DeviceGuard g(device);
-  ECGPU_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_tabs), host.size()));
-  ECGPU_HIP(hipMemcpy(p->d_tabs, host.data(), host.size(), hipMemcpyHostToDevice));
+  if (int rc = plan_upload_tables(p, std::move(host))) return rc;
   p->d_q = reinterpret_cast<u32x4*>(p->d_tabs);
   p->d_p3 = reinterpret_cast<uint32_t*>(p->d_tabs + qb);
   p->d_nib = p->d_tabs + qb + pb;
@@ -285,6 +352,10 @@ int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* co
               hipStream_t stream, bool keep_alive) {
   const size_t ns = size_t(stripes) * p->nsrc, nd = size_t(stripes) * p->rows;
   DeviceGuard g(p->device);
+  // a blocking bind settles the table upload too (it overlapped the table
+  // build-up to here); a bind on a stream leaves it to the launch
+  if (!stream)
+    if (int rc = plan_sync_tables(p)) return rc;
   if (ns + nd > p->cap_ptrs) {
     if (p->d_ptrs) ECGPU_HIP(hipFree(p->d_ptrs));
     p->d_ptrs = nullptr;
@@ -434,6 +505,7 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
 int plan_launch(ecgpu_plan* p, hipStream_t stream) {
   if (p->stripes <= 0 || p->size <= 0 || p->rows <= 0) return ECGPU_OK;
   DeviceGuard g(p->device);
+  if (int rc = plan_wait_tables(p, stream)) return rc;
   if (p->w != 8) return plan_launch_wide(p, stream);
   const int K = p->nsrc;
   const int64_t nvec = p->aligned ? p->size / 16 : 0;

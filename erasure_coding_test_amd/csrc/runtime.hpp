@@ -49,6 +49,12 @@ struct ecgpu_plan {
   size_t cap_ptrs = 0;
   const uint8_t** d_src = nullptr;
   uint8_t** d_dst = nullptr;
+  // the coefficient tables go up asynchronously on the device's upload
+  // stream (plan_init); launches wait for `uploaded` until it has completed.
+  // host_tabs is the copy's source, kept until then.
+  hipEvent_t uploaded = nullptr;
+  bool upload_pending = false;
+  std::vector<uint8_t> host_tabs;
 };
 
 ECGPU_RT_BEGIN

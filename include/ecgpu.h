@@ -153,7 +153,10 @@ ECGPU_API int ecgpu_jerasure_get_stats(double* fill_in);
  * to a table of device pointers for `stripes` stripes:
  *     dst[s][r] = XOR_j coefs[r][j] * src[s][j]   over `size` bytes.
  * Launches are asynchronous on the given hipStream_t (NULL = default stream)
- * and graph-capturable once bound.  SURVEY.md §8b "batched device API". */
+ * and graph-capturable once bound.  ecgpu_plan_create enqueues the
+ * coefficient-table upload on a per-device stream and returns; ecgpu_plan_bind
+ * (blocking) waits for it, so a bound plan's launches never wait on the host.
+ * SURVEY.md §8b "batched device API". */
 typedef struct ecgpu_plan ecgpu_plan;
 ECGPU_API ecgpu_plan* ecgpu_plan_create(int rows, int nsrc, const int* coefs, int device);
 ECGPU_API int ecgpu_plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src_ptrs, uint8_t* const* dst_ptrs,

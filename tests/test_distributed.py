@@ -3,8 +3,11 @@
 Stripes are independent, so ranks shard them round-robin with no data-path
 collective; the only cross-rank operations are the timing
 barrier and the max-reduce of elapsed time.  Each rank here codes its own
-stripes with the CPU oracle (test infrastructure) and the union is checked
-against a single-process run: every stripe coded exactly once, identical bytes.
+stripes with the CPU oracle (test infrastructure: no GPU in this container)
+and the union is checked against a single-process run: every stripe coded
+exactly once, identical bytes.  The same ranks coding with the product
+library on a GPU, and bench.py --gpus 2 itself, are in
+tests/test_multirank_gpu.py (-m gpu).
 """
 import os
 import socket

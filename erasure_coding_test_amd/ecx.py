@@ -7,9 +7,11 @@ per-accumulator first-touch flags (init[]).  ``ParityAccumulator`` keeps the
 m accumulators on the GPU: each ``add`` is one fused launch (only the block
 crosses PCIe when it is in host memory), and ``read`` copies a finished
 parity block out once.  Same byte results as the reference loop.
-``add(..., wait=False)`` only queues the block (its copy overlaps the previous
-block's update); ``sync()`` -- or any read / reset / synchronous add --
-waits for the queued adds and releases their blocks.
+``add(..., wait=False)`` only queues the block's update: a pinned block is read
+in place by the update kernel over PCIe, and consecutive queued adds run back
+to back on the accumulator's stream with no host round trip. ``sync()``, or
+any read, reset or synchronous add, waits for the queued adds and releases
+their blocks.
 """
 from __future__ import annotations
 

@@ -5,7 +5,9 @@ H2D copy, the encode and the D2H copy of consecutive stripes overlapped on
 three HIP streams (ecgpu_pipeline_* in include/ecgpu.h).  ``submit`` returns
 a ticket immediately; the buffers must stay untouched until ``wait(ticket)``.
 Pinned buffers (torch ``pin_memory()`` or :func:`host_register`) get
-asynchronous DMA; pageable ones are staged by HIP.
+asynchronous DMA. Pageable ones are staged by HIP, whose pageable copies
+block the thread that issues them. So the D2H into pageable outputs is issued
+by the pipeline's own worker thread, overlapping the next stripe's H2D.
 
 ``HostPipeline.decoder`` is the read path (client_main.cpp:2055-2182, decode
 after recv): the fused map of jerasure_matrix_decode for one erasure pattern;

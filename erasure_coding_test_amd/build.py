@@ -40,7 +40,7 @@ HDRS = ["gf_host.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "g
 DROPIN_SRCS = ["jerasure_dropin.cpp", "jerasure_surface.cpp"]
 
 CXXFLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", f"-I{INCLUDE}", f"-I{CSRC}"]
-HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
+HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wextra", "-Wno-unused-parameter", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
             "-Wno-unused-result"]
 
 

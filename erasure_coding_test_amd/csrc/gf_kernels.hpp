@@ -782,7 +782,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_perm_generic(ApplyArgs a) {
 
 // --------------------------------------- bytes: tails, misaligned shards ----
 // One lane per byte in [byte0, size); any K, R <= kMaxRows, any alignment.
-static __global__ __launch_bounds__(kBlock) void gf_apply_bytes(ApplyArgs a) {
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void gf_apply_bytes(ApplyArgs a) {
   const int64_t x = a.byte0 + int64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (x >= a.size) return;
   const int s = blockIdx.y;
@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets16p(PacketArgs a) {
 }
 
 // Byte form for packet sizes / bases that are not 8-byte aligned.
-static __global__ __launch_bounds__(kBlock) void gf_xor_packets_bytes(PacketArgs a) {
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void gf_xor_packets_bytes(PacketArgs a) {
   const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (g >= a.ncols) return;
   int64_t sp, col;

@@ -908,7 +908,221 @@ int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, cons
   return ECGPU_OK;
 }
 
-// Runs a fused op synchronously over `size` bytes of every buffer.
+// Where every distinct buffer of one synchronous call lives: sources first
+// (as op.srcs), then the outputs that are not also sources.  devp[i] is the
+// device address the kernel uses (the buffer itself, its mapping in place, or
+// a staging slot); staged[i] marks host memory that must be copied.
+struct CallMap {
+  std::vector<void*> bufs;
+  std::vector<uint8_t*> devp;
+  std::vector<char> staged;
+  size_t nstage = 0;
+  size_t slot = 0;   // staging slot bytes (size rounded to 256)
+  int64_t size = 0;
+  int rows = 0, nsrc = 0;
+  bool host_io = false;  // some buffer is host memory the kernel uses in place
+  size_t index(const void* p) const { return size_t(std::find(bufs.begin(), bufs.end(), p) - bufs.begin()); }
+  std::vector<const uint8_t*> sources() const { return {devp.begin(), devp.begin() + nsrc}; }
+  std::vector<uint8_t*> outputs(const FusedOp& op) const {
+    std::vector<uint8_t*> dp(static_cast<size_t>(rows));
+    for (int r = 0; r < rows; ++r) dp[size_t(r)] = devp[index(op.dsts[size_t(r)])];
+    return dp;
+  }
+};
+
+int map_buffers(const FusedOp& op, int64_t size, int device, bool inl, CallMap* m) {
+  m->bufs = op.srcs;
+  for (void* d : op.dsts)
+    if (std::find(m->bufs.begin(), m->bufs.end(), d) == m->bufs.end()) m->bufs.push_back(d);
+  m->size = size;
+  m->slot = (size_t(size) + 255) & ~size_t(255);
+  m->rows = int(op.dsts.size());
+  m->nsrc = int(op.srcs.size());
+  m->devp.assign(m->bufs.size(), nullptr);
+  m->staged.assign(m->bufs.size(), 0);
+  for (size_t i = 0; i < m->bufs.size(); ++i) {
+    bool on_dev = false;
+    if (int rc = classify(m->bufs[i], device, &on_dev)) return rc;
+    if (on_dev) {
+      m->devp[i] = static_cast<uint8_t*>(m->bufs[i]);
+    } else {
+      m->staged[i] = 1;
+      ++m->nstage;
+    }
+  }
+  if (inl && zero_copy_pinned()) {
+    // pinned / registered host buffers are read and written by the kernel in
+    // place over PCIe: no staging copy, no DMA setup, and a call's reads and
+    // writes overlap on the two directions of the link
+    for (size_t i = 0; i < m->bufs.size(); ++i) {
+      void* d = nullptr;
+      if (m->staged[i] && host_mapped(m->bufs[i], size_t(size), &d)) {
+        m->staged[i] = 0;
+        --m->nstage;
+        m->devp[i] = static_cast<uint8_t*>(d);
+        m->host_io = true;
+      }
+    }
+  }
+  return ECGPU_OK;
+}
+
+int launch_and_sync(Ctx* c, const FusedOp& op, const CallMap& m, bool host_io) {
+  if (int rc = launch_inline(op, m.sources(), m.outputs(op), m.size, c->stream, host_io)) return rc;
+  ECGPU_HIP(hipStreamSynchronize(c->stream));
+  ECGPU_HIP(hipGetLastError());
+  return ECGPU_OK;
+}
+
+// Small calls: every staged buffer goes through coherent pinned memory the
+// kernel reads and writes in place -- host copies and ONE launch, no DMA.
+int exec_zero_copy(Ctx* c, const FusedOp& op, CallMap& m) {
+  if (int rc = ensure_zc(c, m.nstage * m.slot)) return rc;
+  size_t next = 0;
+  for (size_t i = 0; i < m.bufs.size(); ++i)
+    if (m.staged[i]) m.devp[i] = c->zc + (next++) * m.slot;
+  for (int j = 0; j < m.nsrc; ++j)
+    if (m.staged[size_t(j)]) std::memcpy(m.devp[size_t(j)], op.srcs[size_t(j)], size_t(m.size));
+  if (int rc = launch_and_sync(c, op, m, /*host_io=*/true)) return rc;
+  for (int r = 0; r < m.rows; ++r) {
+    const size_t i = m.index(op.dsts[size_t(r)]);
+    if (m.staged[i]) std::memcpy(op.dsts[size_t(r)], m.devp[i], size_t(m.size));
+  }
+  return ECGPU_OK;
+}
+
+// Larger calls with few output bytes: sources cross by HIP's copies (a
+// contiguous pageable run goes as one pinned blit at link rate), the kernel
+// writes the outputs straight into coherent pinned memory and the calling
+// thread copies them out: no per-output pageable D2H (67 us per 1 MiB shard,
+// tools/pageable_duplex_probe.cpp).  Returns ECGPU_OK with *done = false when
+// the call does not qualify (an output that is also a source, or outputs
+// above zc_out_max() / zc_out_shard_max()).
+int exec_outputs_zero_copy(Ctx* c, const FusedOp& op, CallMap& m, bool* done) {
+  *done = false;
+  size_t nout = 0;
+  std::vector<char> is_out(m.bufs.size(), 0);
+  for (int r = 0; r < m.rows; ++r) {
+    const size_t i = m.index(op.dsts[size_t(r)]);
+    if (!m.staged[i] || is_out[i]) continue;
+    if (i < size_t(m.nsrc)) return ECGPU_OK;  // aliased: keep the staged path
+    is_out[i] = 1;
+    ++nout;
+  }
+  if (nout == 0 || nout * size_t(m.size) > zc_out_max() || size_t(m.size) > zc_out_shard_max()) return ECGPU_OK;
+  const size_t nin = m.nstage - nout;
+  if (int rc = ensure_zc(c, nout * m.slot)) return rc;
+  if (int rc = ensure_stage(c, std::max<size_t>(nin, 1) * m.slot)) return rc;
+  size_t ni = 0, no = 0;
+  std::vector<char*> staged_hp;
+  for (size_t i = 0; i < m.bufs.size(); ++i) {
+    if (!m.staged[i]) continue;
+    if (is_out[i]) {
+      m.devp[i] = c->zc + (no++) * m.slot;
+    } else {
+      m.devp[i] = c->stage + (ni++) * m.slot;
+      staged_hp.push_back(static_cast<char*>(m.bufs[i]));
+    }
+  }
+  if (int rc = copy_shards(true, c->stage, m.slot, staged_hp, size_t(m.size), c->stream)) return rc;
+  if (int rc = launch_and_sync(c, op, m, /*host_io=*/true)) return rc;
+  for (size_t i = 0; i < m.bufs.size(); ++i)
+    if (m.staged[i] && is_out[i]) std::memcpy(m.bufs[i], m.devp[i], size_t(m.size));
+  *done = true;
+  return ECGPU_OK;
+}
+
+// Everything else: staged buffers go through the context's HBM slab, by the
+// pinned bounce (mid-size) or HIP's copies (large); non-inline ops (w = 16 /
+// 32, > 16 sources, the LDS engine) run a cached bound plan.
+int exec_staged(Ctx* c, const FusedOp& op, CallMap& m, bool inl) {
+  const size_t slot = m.slot, size = size_t(m.size);
+  const int rows = m.rows, nsrc = m.nsrc;
+  // With several launches (> 4 rows) an output that is also a source must
+  // not be overwritten before the last launch reads it: write to temps.
+  const bool via_temp = op.dst_is_src && rows > dev::kMaxRows;
+  const size_t ntemp = via_temp ? size_t(rows) : 0;
+  if (int rc = ensure_stage(c, (m.nstage + ntemp) * slot)) return rc;
+  size_t next = 0;
+  for (size_t i = 0; i < m.bufs.size(); ++i)
+    if (m.staged[i]) m.devp[i] = c->stage + (next++) * slot;
+  // Staged sources take the first staging slots (bufs lists sources first),
+  // so with the pinned bounce they go up as one contiguous DMA.
+  const bool bounce = m.nstage > 0 && m.nstage * slot <= bounce_max();
+  if (bounce)
+    if (int rc = ensure_bounce(c, m.nstage * slot)) return rc;
+  auto bounce_of = [&](size_t i) { return c->bounce + (m.devp[i] - c->stage); };
+  std::vector<char*> staged_hp;
+  for (size_t j = 0; j < op.srcs.size(); ++j)
+    if (m.staged[j]) {
+      staged_hp.push_back(static_cast<char*>(op.srcs[j]));
+      if (bounce) std::memcpy(bounce_of(j), op.srcs[j], size);
+    }
+  if (bounce && !staged_hp.empty()) {
+    ECGPU_HIP(hipMemcpyAsync(c->stage, c->bounce, staged_hp.size() * slot, hipMemcpyHostToDevice, c->stream));
+  } else if (int rc = copy_shards(true, c->stage, slot, staged_hp, size, c->stream)) {
+    return rc;
+  }
+
+  const std::vector<const uint8_t*> sp = m.sources();
+  std::vector<uint8_t*> dp = m.outputs(op);
+  if (via_temp)
+    for (int r = 0; r < rows; ++r) dp[size_t(r)] = c->stage + (m.nstage + size_t(r)) * slot;
+  if (nsrc == 0) {
+    // Every output is identically zero (e.g. region multiply by 0 without
+    // add, galois.cpp:447-451): nothing to read.
+    for (int r = 0; r < rows; ++r) ECGPU_HIP(hipMemsetAsync(dp[size_t(r)], 0, size, c->stream));
+  } else if (inl) {
+    if (int rc = launch_inline(op, sp, dp, m.size, c->stream, m.host_io)) return rc;
+  } else {
+    ecgpu_plan* p = nullptr;
+    if (int rc = ctx_plan(c, rows, nsrc, op.coef, op.w, &p)) return rc;
+    // sp/dp outlive the stream sync below
+    if (int rc = plan_bind(p, 1, sp.data(), dp.data(), m.size, c->stream, /*keep_alive=*/true)) return rc;
+    if (int rc = plan_launch(p, c->stream)) return rc;
+  }
+  // staged outputs, in slot order
+  std::vector<std::pair<uint8_t*, char*>> outs;  // (device slot, host pointer)
+  for (int r = 0; r < rows; ++r) {
+    const size_t i = m.index(op.dsts[size_t(r)]);
+    if (via_temp)
+      ECGPU_HIP(hipMemcpyAsync(m.devp[i], dp[size_t(r)], size, hipMemcpyDeviceToDevice, c->stream));
+    if (m.staged[i]) outs.emplace_back(m.devp[i], static_cast<char*>(op.dsts[size_t(r)]));
+  }
+  std::sort(outs.begin(), outs.end());
+  if (bounce) {
+    // one D2H per run of adjacent slots (the bounce mirrors the slab)
+    for (size_t a = 0; a < outs.size();) {
+      size_t b = a + 1;
+      while (b < outs.size() && outs[b].first == outs[b - 1].first + slot) ++b;
+      const size_t off = size_t(outs[a].first - c->stage);
+      ECGPU_HIP(hipMemcpyAsync(c->bounce + off, outs[a].first, (b - a - 1) * slot + size, hipMemcpyDeviceToHost,
+                               c->stream));
+      a = b;
+    }
+    ECGPU_HIP(hipStreamSynchronize(c->stream));
+    ECGPU_HIP(hipGetLastError());
+    for (const auto& o : outs) std::memcpy(o.second, c->bounce + (o.first - c->stage), size);
+    return ECGPU_OK;
+  }
+  // outputs in consecutive slots: one 2-D copy per evenly spaced run of host outputs
+  bool consecutive = true;
+  for (size_t i = 1; i < outs.size() && consecutive; ++i) consecutive = outs[i].first == outs[0].first + i * slot;
+  if (consecutive && !outs.empty()) {
+    std::vector<char*> hp;
+    for (const auto& o : outs) hp.push_back(o.second);
+    if (int rc = copy_shards(false, outs[0].first, slot, hp, size, c->stream)) return rc;
+  } else {
+    for (const auto& o : outs) ECGPU_HIP(hipMemcpyAsync(o.second, o.first, size, hipMemcpyDeviceToHost, c->stream));
+  }
+  ECGPU_HIP(hipStreamSynchronize(c->stream));
+  ECGPU_HIP(hipGetLastError());
+  return ECGPU_OK;
+}
+
+// Runs a fused op synchronously over `size` bytes of every buffer: maps the
+// buffers, then the cheapest staging mode for the host ones (§8 of DESIGN.md;
+// the thresholds are measured, see bounce_max / zc_max / zc_out_max).
 int execute(const FusedOp& op, int64_t size) {
   if (op.w != 8 && size % (op.w / 8) != 0)
     return fail(ECGPU_ERR_ARG, "w = " + std::to_string(op.w) + ": size must be a multiple of the word size");
@@ -919,194 +1133,16 @@ int execute(const FusedOp& op, int64_t size) {
   if (!lease.c) return lease.rc;
   Ctx* c = lease.c;
   DeviceGuard g(device);
-
-  // Map every distinct buffer to a device address (in place or a staging slot).
-  std::vector<void*> bufs = op.srcs;
-  for (void* d : op.dsts)
-    if (std::find(bufs.begin(), bufs.end(), d) == bufs.end()) bufs.push_back(d);
-  const size_t slot = (size_t(size) + 255) & ~size_t(255);
-  std::vector<uint8_t*> devp(bufs.size(), nullptr);
-  std::vector<char> staged(bufs.size(), 0);
-  size_t nstage = 0;
-  for (size_t i = 0; i < bufs.size(); ++i) {
-    bool on_dev = false;
-    int rc = classify(bufs[i], device, &on_dev);
-    if (rc != ECGPU_OK) return rc;
-    if (on_dev) {
-      devp[i] = static_cast<uint8_t*>(bufs[i]);
-    } else {
-      staged[i] = 1;
-      ++nstage;
-    }
-  }
-  const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
-  auto buf_index = [&](void* p) { return size_t(std::find(bufs.begin(), bufs.end(), p) - bufs.begin()); };
   const bool inl = inline_ok(op);
-  bool host_io = false;  // some buffer is used in place in host memory
-  if (inl && zero_copy_pinned()) {
-    // pinned / registered host buffers are read and written by the kernel in
-    // place over PCIe: no staging copy, no DMA setup, and a call's reads and
-    // writes overlap on the two directions of the link
-    for (size_t i = 0; i < bufs.size(); ++i) {
-      void* d = nullptr;
-      if (staged[i] && host_mapped(bufs[i], size_t(size), &d)) {
-        staged[i] = 0;
-        --nstage;
-        devp[i] = static_cast<uint8_t*>(d);
-        host_io = true;
-      }
-    }
+  CallMap m;
+  if (int rc = map_buffers(op, size, device, inl, &m)) return rc;
+  if (inl && m.nstage > 0 && m.nstage * size_t(size) <= zc_max()) return exec_zero_copy(c, op, m);
+  if (inl && m.nstage > 0 && m.nstage * m.slot > bounce_max()) {
+    bool done = false;
+    if (int rc = exec_outputs_zero_copy(c, op, m, &done)) return rc;
+    if (done) return ECGPU_OK;
   }
-
-  // --- small calls: zero-copy through coherent pinned memory, one launch ---
-  if (inl && nstage > 0 && nstage * size_t(size) <= zc_max()) {
-    if (int rc = ensure_zc(c, nstage * slot)) return rc;
-    size_t next = 0;
-    for (size_t i = 0; i < bufs.size(); ++i)
-      if (staged[i]) devp[i] = c->zc + (next++) * slot;
-    for (int j = 0; j < nsrc; ++j)
-      if (staged[size_t(j)]) std::memcpy(devp[size_t(j)], op.srcs[size_t(j)], size_t(size));
-    std::vector<const uint8_t*> sp(devp.begin(), devp.begin() + nsrc);
-    std::vector<uint8_t*> dp(static_cast<size_t>(rows));
-    for (int r = 0; r < rows; ++r) dp[size_t(r)] = devp[buf_index(op.dsts[size_t(r)])];
-    if (int rc = launch_inline(op, sp, dp, size, c->stream, /*host_io=*/true)) return rc;
-    ECGPU_HIP(hipStreamSynchronize(c->stream));
-    ECGPU_HIP(hipGetLastError());
-    for (int r = 0; r < rows; ++r) {
-      const size_t i = buf_index(op.dsts[size_t(r)]);
-      if (staged[i]) std::memcpy(op.dsts[size_t(r)], devp[i], size_t(size));
-    }
-    return ECGPU_OK;
-  }
-
-  // --- larger calls with few output bytes: sources cross by HIP's copies
-  // (a contiguous pageable run goes as one pinned blit at link rate), the
-  // kernel writes the outputs straight into coherent pinned memory and the
-  // calling thread copies them out: no per-output pageable D2H (67 us per
-  // 1 MiB shard, tools/pageable_duplex_probe.cpp).  Outputs that are also
-  // sources keep the staged path.
-  if (inl && nstage > 0 && nstage * slot > bounce_max()) {
-    size_t nout = 0;
-    bool aliased = false;
-    std::vector<char> is_out(bufs.size(), 0);
-    for (int r = 0; r < rows; ++r) {
-      const size_t i = buf_index(op.dsts[size_t(r)]);
-      if (!staged[i] || is_out[i]) continue;
-      is_out[i] = 1;
-      aliased = aliased || i < size_t(nsrc);
-      ++nout;
-    }
-    if (!aliased && nout > 0 && nout * size_t(size) <= zc_out_max() && size_t(size) <= zc_out_shard_max()) {
-      const size_t nin = nstage - nout;
-      if (int rc = ensure_zc(c, nout * slot)) return rc;
-      if (int rc = ensure_stage(c, std::max<size_t>(nin, 1) * slot)) return rc;
-      size_t ni = 0, no = 0;
-      std::vector<char*> staged_hp;
-      for (size_t i = 0; i < bufs.size(); ++i) {
-        if (!staged[i]) continue;
-        if (is_out[i]) {
-          devp[i] = c->zc + (no++) * slot;
-        } else {
-          devp[i] = c->stage + (ni++) * slot;
-          staged_hp.push_back(static_cast<char*>(bufs[i]));
-        }
-      }
-      if (int rc = copy_shards(true, c->stage, slot, staged_hp, size_t(size), c->stream)) return rc;
-      std::vector<const uint8_t*> sp(devp.begin(), devp.begin() + nsrc);
-      std::vector<uint8_t*> dp(static_cast<size_t>(rows));
-      for (int r = 0; r < rows; ++r) dp[size_t(r)] = devp[buf_index(op.dsts[size_t(r)])];
-      if (int rc = launch_inline(op, sp, dp, size, c->stream, /*host_io=*/true)) return rc;
-      ECGPU_HIP(hipStreamSynchronize(c->stream));
-      ECGPU_HIP(hipGetLastError());
-      for (size_t i = 0; i < bufs.size(); ++i)
-        if (staged[i] && is_out[i]) std::memcpy(bufs[i], devp[i], size_t(size));
-      return ECGPU_OK;
-    }
-  }
-
-  // With several launches (> 4 rows) an output that is also a source must
-  // not be overwritten before the last launch reads it: write to temps.
-  const bool via_temp = op.dst_is_src && rows > dev::kMaxRows;
-  const size_t ntemp = via_temp ? size_t(rows) : 0;
-  int rc = ensure_stage(c, (nstage + ntemp) * slot);
-  if (rc != ECGPU_OK) return rc;
-  size_t next = 0;
-  for (size_t i = 0; i < bufs.size(); ++i)
-    if (staged[i]) devp[i] = c->stage + (next++) * slot;
-  // Staged sources take the first staging slots (bufs lists sources first),
-  // so with the pinned bounce they go up as one contiguous DMA.
-  const bool bounce = nstage > 0 && nstage * slot <= bounce_max();
-  if (bounce && (rc = ensure_bounce(c, nstage * slot)) != ECGPU_OK) return rc;
-  auto bounce_of = [&](size_t i) { return c->bounce + (devp[i] - c->stage); };
-  std::vector<char*> staged_hp;
-  for (size_t j = 0; j < op.srcs.size(); ++j)
-    if (staged[j]) {
-      staged_hp.push_back(static_cast<char*>(op.srcs[j]));
-      if (bounce) std::memcpy(bounce_of(j), op.srcs[j], size_t(size));
-    }
-  if (bounce && !staged_hp.empty())
-    ECGPU_HIP(hipMemcpyAsync(c->stage, c->bounce, staged_hp.size() * slot, hipMemcpyHostToDevice, c->stream));
-  else if ((rc = copy_shards(true, c->stage, slot, staged_hp, size_t(size), c->stream)) != ECGPU_OK)
-    return rc;
-
-  std::vector<const uint8_t*> sp(static_cast<size_t>(nsrc));
-  std::vector<uint8_t*> dp(static_cast<size_t>(rows));
-  for (int j = 0; j < nsrc; ++j) sp[j] = devp[j];
-  for (int r = 0; r < rows; ++r)
-    dp[r] = via_temp ? c->stage + (nstage + size_t(r)) * slot : devp[buf_index(op.dsts[size_t(r)])];
-  if (nsrc == 0) {
-    // Every output is identically zero (e.g. region multiply by 0 without
-    // add, galois.cpp:447-451): nothing to read.
-    for (int r = 0; r < rows; ++r) ECGPU_HIP(hipMemsetAsync(dp[r], 0, size_t(size), c->stream));
-  } else if (inl) {
-    if ((rc = launch_inline(op, sp, dp, size, c->stream, host_io)) != ECGPU_OK) return rc;
-  } else {
-    ecgpu_plan* p = nullptr;
-    rc = ctx_plan(c, rows, nsrc, op.coef, op.w, &p);
-    if (rc != ECGPU_OK) return rc;
-    rc = plan_bind(p, 1, sp.data(), dp.data(), size, c->stream, /*keep_alive=*/true);  // sp/dp outlive the sync below
-    if (rc != ECGPU_OK) return rc;
-    rc = plan_launch(p, c->stream);
-    if (rc != ECGPU_OK) return rc;
-  }
-  // staged outputs, in slot order
-  std::vector<std::pair<uint8_t*, char*>> outs;  // (device slot, host pointer)
-  for (int r = 0; r < rows; ++r) {
-    const size_t i = buf_index(op.dsts[size_t(r)]);
-    if (via_temp)
-      ECGPU_HIP(hipMemcpyAsync(devp[i], dp[r], size_t(size), hipMemcpyDeviceToDevice, c->stream));
-    if (staged[i]) outs.emplace_back(devp[i], static_cast<char*>(op.dsts[size_t(r)]));
-  }
-  std::sort(outs.begin(), outs.end());
-  if (bounce) {
-    // one D2H per run of adjacent slots (the bounce mirrors the slab)
-    for (size_t a = 0; a < outs.size();) {
-      size_t b = a + 1;
-      while (b < outs.size() && outs[b].first == outs[b - 1].first + slot) ++b;
-      const size_t off = size_t(outs[a].first - c->stage);
-      ECGPU_HIP(hipMemcpyAsync(c->bounce + off, outs[a].first, (b - a - 1) * slot + size_t(size),
-                               hipMemcpyDeviceToHost, c->stream));
-      a = b;
-    }
-    ECGPU_HIP(hipStreamSynchronize(c->stream));
-    ECGPU_HIP(hipGetLastError());
-    for (const auto& o : outs) std::memcpy(o.second, c->bounce + (o.first - c->stage), size_t(size));
-    return ECGPU_OK;
-  }
-  // outputs in consecutive slots: one 2-D copy per evenly spaced run of host outputs
-  bool consecutive = true;
-  for (size_t i = 1; i < outs.size() && consecutive; ++i) consecutive = outs[i].first == outs[0].first + i * slot;
-  if (consecutive && !outs.empty()) {
-    std::vector<char*> hp;
-    for (const auto& o : outs) hp.push_back(o.second);
-    if ((rc = copy_shards(false, outs[0].first, slot, hp, size_t(size), c->stream)) != ECGPU_OK) return rc;
-  } else {
-    for (const auto& o : outs)
-      ECGPU_HIP(hipMemcpyAsync(o.second, o.first, size_t(size), hipMemcpyDeviceToHost, c->stream));
-  }
-  ECGPU_HIP(hipStreamSynchronize(c->stream));
-  ECGPU_HIP(hipGetLastError());
-  return ECGPU_OK;
+  return exec_staged(c, op, m, inl);
 }
 
 ECGPU_RT_END

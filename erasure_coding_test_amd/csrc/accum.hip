@@ -170,9 +170,11 @@ ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int
     for (void* p : op.dsts) dp.push_back(static_cast<uint8_t*>(p));
     if (int rc = launch_inline(op, sp, dp, a->size, a->stream, /*host_io=*/in_place)) return rc;
   } else {
-    // engine override or > 4 aliased rows: the synchronous path
+    // engine override or > 4 aliased rows: the synchronous path, which
+    // classifies and maps host memory itself -- so it gets the caller's
+    // pointer, not the device alias of a pinned block
     if (int rc = accum_sync(a)) return rc;
-    if (int rc = execute(op, a->size)) return rc;
+    if (int rc = execute(in_place ? accum_op(a, block, coefs) : op, a->size)) return rc;
   }
   for (int i = 0; i < a->m; ++i)
     if (coefs[i] & 0xFF) a->init[i] = 1;

@@ -38,6 +38,7 @@
 #include "gf_host.hpp"
 #include "gf_kernels.hpp"
 #include "gf_spec.hpp"
+#include "host_sync.hpp"
 #include "matrix_host.hpp"
 #include "planner.hpp"
 #include "runtime.hpp"
@@ -218,17 +219,12 @@ ECGPU_RT_BEGIN
 // creation does not wait for its tables (one blocking copy cost ~12 us,
 // tools/hip_overheads.cpp); its launches wait on the upload's event instead.
 hipStream_t upload_stream(int device) {
-  static std::mutex mu;
-  static std::vector<hipStream_t> streams;
-  std::lock_guard<std::mutex> lk(mu);
-  if (size_t(device) >= streams.size()) streams.resize(size_t(device) + 1, nullptr);
-  if (!streams[size_t(device)]) {
-    DeviceGuard g(device);
+  static hostsync::PerDevice<hipStream_t> streams;
+  return streams.get(device, [](int dev) {
+    DeviceGuard g(dev);
     hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    streams[size_t(device)] = s;
-  }
-  return streams[size_t(device)];
+    return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? s : nullptr;
+  });
 }
 
 // Allocates p->d_tabs and uploads `host` into it without waiting (the plan
@@ -571,8 +567,7 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
 
 // ------------------------------------------------------ context pool ----
 
-std::mutex g_pool_mu;
-std::vector<Ctx*> g_pool;  // idle contexts; never destroyed (process lifetime)
+hostsync::IdlePool<Ctx> g_pool;  // idle contexts (process lifetime)
 
 int current_device() {
   const int forced = env_int("ECGPU_DEVICE", -1);
@@ -583,15 +578,9 @@ int current_device() {
 }
 
 Ctx* acquire_ctx(int device, int* rc) {
-  {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    for (size_t i = 0; i < g_pool.size(); ++i)
-      if (g_pool[i]->device == device) {
-        Ctx* c = g_pool[i];
-        g_pool.erase(g_pool.begin() + long(i));
-        *rc = ECGPU_OK;
-        return c;
-      }
+  if (Ctx* c = g_pool.acquire(device)) {
+    *rc = ECGPU_OK;
+    return c;
   }
   auto* c = new Ctx();
   c->device = device;
@@ -611,10 +600,7 @@ Ctx* acquire_ctx(int device, int* rc) {
   return c;
 }
 
-void release_ctx(Ctx* c) {
-  std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool.push_back(c);
-}
+void release_ctx(Ctx* c) { g_pool.release(c->device, c); }
 
 
 int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int w, ecgpu_plan** out) {

@@ -580,6 +580,71 @@ def test_host_pipeline_mixed_output_memory(ec, gpu, restatement, pattern):
             assert (got[size:] == 0x77).all(), (s, i)
 
 
+@pytest.fixture
+def d2h_worker_delay():
+    """ECGPU_TEST_D2H_DELAY_US: the pipeline's D2H worker sleeps 3 ms between
+    taking a job and issuing it (read when a pipeline is created)."""
+    old = os.environ.get("ECGPU_TEST_D2H_DELAY_US")
+    os.environ["ECGPU_TEST_D2H_DELAY_US"] = "3000"
+    yield
+    if old is None:
+        del os.environ["ECGPU_TEST_D2H_DELAY_US"]
+    else:
+        os.environ["ECGPU_TEST_D2H_DELAY_US"] = old
+
+
+@pytest.mark.parametrize("pattern", ["alternate", "pageable_then_pinned"])
+@pytest.mark.parametrize("depth", [1, 2])
+def test_host_pipeline_wait_is_exact_with_delayed_worker(ec, gpu, restatement, d2h_worker_delay, pattern, depth):
+    """Round-2 race: with pinned inputs, a pinned-output
+    stripe following a pageable one used to be issued inline while the D2H
+    worker still held the pageable job, so wait() on the earlier ticket could
+    return before its outputs landed, its slot could be reused under the
+    copy, and drain() could hang.  The worker's delay makes that window 3 ms
+    wide on every run.  Each stripe is checked against the oracle right after
+    wait(t) -- before the next submit can reuse its slot -- and the last
+    stripe is pinned after a pageable one, so drain() must return."""
+    import threading
+
+    import torch
+    k, m, size, stripes = 6, 3, (1 << 20) + 16, 8
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    data = [[torch.from_numpy(b).pin_memory() for b in host_shards(71, s, k, size)] for s in range(stripes)]
+
+    def pinned_at(s):
+        return s % 2 == 1 if pattern == "alternate" else s == stripes - 1
+
+    coding = [[torch.full((size + PAD,), 0x77, dtype=torch.uint8).pin_memory() for _ in range(m)] if pinned_at(s)
+              else [np.full(size + PAD, 0x77, np.uint8) for _ in range(m)] for s in range(stripes)]
+    assert pinned_at(stripes - 1) and not pinned_at(stripes - 2)
+    refs = [_encode_ref(restatement, k, m, M, [b.numpy() for b in data[s]], size) for s in range(stripes)]
+
+    def check(s):
+        for i in range(m):
+            got = coding[s][i].numpy() if hasattr(coding[s][i], "numpy") else coding[s][i]
+            assert np.array_equal(got[:size], refs[s][i][:size]), (s, i)
+            assert (got[size:] == 0x77).all(), (s, i)
+
+    p = ec.HostPipeline(k, m, M, size, depth=depth)
+    try:
+        prev = None
+        for s in range(stripes):
+            t = p.submit(data[s], coding[s])
+            assert t == s
+            if prev is not None:
+                p.wait(prev)  # the ticket before: its slot is reused by the next submit at depth 2
+                check(prev)
+            prev = t
+        done = threading.Event()
+        th = threading.Thread(target=lambda: (p.drain(), done.set()), daemon=True)
+        th.start()
+        th.join(60)
+        assert done.is_set(), "drain() did not return"
+        check(stripes - 1)
+    finally:
+        p.close()
+
+
 @pytest.mark.parametrize("pinned", [True, False])
 @pytest.mark.parametrize("pitch_pad", [0, 4096 + 3])
 def test_host_pipeline_stripe_slab(ec, gpu, restatement, pinned, pitch_pad):
@@ -731,16 +796,19 @@ def test_pipeline_group_encode_round_robin(ec, gpu, restatement, members, memory
             assert not coding[s][i].numpy()[size:].any()
 
 
-def test_pipeline_group_concurrent_submitters(ec, gpu, restatement):
-    # per-member submit workers, no group-wide lock: four host threads submit
-    # interleaved stripes (pageable and pinned) into one group of three
-    # members and wait on their own tickets out of order
+@pytest.mark.parametrize("members,depth,nthreads", [(3, 2, 4), (1, 1, 6), (2, 1, 8)])
+def test_pipeline_group_concurrent_submitters(ec, gpu, restatement, members, depth, nthreads):
+    # per-member submit workers, no group-wide lock: host threads submit
+    # interleaved stripes (pageable and pinned) into one group and wait on
+    # their own tickets out of order.  More submitters than depth + 1 per
+    # member is the shape of the round-2 lost wake-up (a put of
+    # exactly the worker's next ticket was never re-signalled)
     import threading
 
     import torch
-    k, m, size, per_thread, nthreads = 6, 3, (1 << 17) + 3, 5, 4
+    k, m, size, per_thread = 6, 3, (1 << 17) + 3, 5
     M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
-    g = ec.HostPipelineGroup(k, m, M, size, devices=[0, 0, 0], depth=2)
+    g = ec.HostPipelineGroup(k, m, M, size, devices=[0] * members, depth=depth)
     results, errors = {}, []
 
     def run(tid):

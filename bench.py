@@ -390,29 +390,69 @@ def copy_ceiling(slab, shard, reps: int = 10):
                       f"{'nt' if policy & 2 else 'plain'}), median of {reps}"}
 
 
-def load_traffic(name: str, workload_key: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary
+def load_traffic(name: str, workload_key: str, kernel_id: str, profiles_dir: str = ""):
+    """(HBM bytes per launch, note) from the committed rocprofv3 PMC summary
     (profiles/pmc_<name>.json, written by profiles/summarize.py from separate
-    --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command), or None
-    when the summary is for another workload."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command).  The
+    bytes are given only when the record is for this workload AND for the
+    kernels of the loaded library (its ecgpu_build_id(1), stored in the record
+    as kernel_build_id); otherwise None and the reason."""
+    p = os.path.join(profiles_dir or os.path.join(ROOT, "profiles"), f"pmc_{name}.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload_key") == workload_key:
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
-    return None
+    except (OSError, ValueError) as ex:
+        return None, f"no PMC record ({type(ex).__name__})"
+    if d.get("workload_key") != workload_key:
+        return None, f"PMC record is for workload {d.get('workload_key')}, not {workload_key}"
+    if d.get("kernel_build_id") != kernel_id:
+        return None, (f"PMC record measured kernel build {d.get('kernel_build_id')}, the loaded library is "
+                      f"{kernel_id}: stale, not reported")
+    return d.get("hbm_bytes_per_launch"), f"{d.get('from')} (kernel build {kernel_id})"
+
+
+CFG_WARMUP, CFG_REPS = 5, 20  # per configs-block entry (profiles/summarize.py relies on these counts)
+C3_RANDOM_DATA_ERASURE_SEED = 0xC3
+
+
+def c3_random_data_erasure() -> int:
+    """The seeded single data erasure of the C3 decode shapes (1..k-1; 0 is the
+    timed decode{0})."""
+    import random
+    return random.Random(C3_RANDOM_DATA_ERASURE_SEED).randrange(1, 10)
+
+
+def c3_decode_shapes(E, shards, S, B, dev, stream, kind, nt):
+    """SURVEY.md §8d's other C3 decode shapes, on the timed slab: a lost
+    parity shard (erasure {12}: the dense re-encode of row 2 from the data,
+    jerasure.cpp:243-247) and a seeded single data erasure (jerasure.cpp:223-228;
+    rebuilt from the other data shards and parity 0, whose Vandermonde row is
+    all ones, so it is XOR-only like decode{0}).  Each rewrites its shard with
+    the same bytes, so the slab stays a consistent stripe."""
+    k, m = 10, 4
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    out = {}
+    j = c3_random_data_erasure()
+    for name, er, what in (("C3_decode_data_random", [j], f"erasure {{{j}}} (seeded single data shard; XOR-only)"),
+                           ("C3_decode_parity", [k + 2], "erasure {12} (lost parity: dense re-encode of row 2)")):
+        dp = E.DecodePlan(k, m, M, er, 0, dev.index).bind_stripes(shards, S)
+        dp.set_kernel(kind, nt)
+        ms = time_launches(lambda: dp.launch(stream.cuda_stream), stream, CFG_REPS, warmup=CFG_WARMUP)
+        e = {"workload": f"RS(10,4) decode of {what}, 4 MiB shards, {B} stripes (10 shards read, 1 written)"}
+        e.update(roofline_entry((k + 1) * S * B, ms))
+        out[name] = e
+        dp.close()
+    return out
 
 
 def config_block(E, N, dev, stream, kind, nt, main=None):
     """Every BASELINE.json GPU config as its own launch (median of 20 HIP-event
     timed launches after warm-up; batches sized to 4.5-6.5 GB streamed per
     launch, like the timed C3 steps' 5.6 GB, so launch ramp and tail weigh
-    the same in every config): C2 encode,
-    C3 encode / decode{0} (from the timed steps), C4 decode{0,1,2,3} with its
-    host-side plan cost reported separately, C5 encode."""
+    the same in every config): C2 encode, C3 encode / decode{0} (from the
+    timed steps) and its other decode shapes (`main`, c3_decode_shapes),
+    C4 decode{0,1,2,3} with its host-side plan cost reported separately
+    (SURVEY.md §8d), C5 encode.  Runs on every rank, on its own GPU."""
     import ctypes
 
     import torch
@@ -424,7 +464,7 @@ def config_block(E, N, dev, stream, kind, nt, main=None):
         fill_random(slab, list(range(B)), cfg_id)
         p = E.encode_plan(k, m, M, dev.index).bind([st[:k] for st in shards], [st[k:] for st in shards], S)
         p.set_kernel(kind, nt)
-        ms = time_launches(lambda: p.launch(stream.cuda_stream), stream, 20, warmup=5)
+        ms = time_launches(lambda: p.launch(stream.cuda_stream), stream, CFG_REPS, warmup=CFG_WARMUP)
         e = {"workload": f"RS({k},{m}) encode, {S >> 20} MiB shards, {B} stripes"}
         e.update(roofline_entry((k + m) * S * B, ms))
         out[name] = e
@@ -460,7 +500,7 @@ def config_block(E, N, dev, stream, kind, nt, main=None):
         dp.close()
     dp = E.DecodePlan(k, m, M, er, 0, dev.index).bind_stripes(shards, S)
     dp.set_kernel(kind, nt)
-    ms = time_launches(lambda: dp.launch(stream.cuda_stream), stream, 20, warmup=5)
+    ms = time_launches(lambda: dp.launch(stream.cuda_stream), stream, CFG_REPS, warmup=CFG_WARMUP)
     e = {"workload": f"RS(10,4) decode of erasures {{0,1,2,3}}, 4 MiB shards, {B} stripes (10 survivors read, "
                      f"4 shards written)"}
     e.update(roofline_entry((k + len(er)) * S * B, ms))
@@ -530,6 +570,7 @@ def main(argv=None):
     # shard stride (S + 10 KiB skew); global stripe ids round-robin over ranks
     ids = global_stripe_ids(B, rank, world)
     slab, shards = E.alloc_stripes(B, k, m, S, dev)
+    shard_stride = int(slab.stride(1))
     fill_random(slab, ids, C["cfg_id"])
 
     kind = N.KERNEL_LDS if args.kernel == "lds" else N.KERNEL_PERM
@@ -541,27 +582,34 @@ def main(argv=None):
         dec.set_kernel(kind, bool(args.nt))
     stream = torch.cuda.current_stream(dev)
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
+    # HIP events on the launch stream, one per kernel boundary: event 0 opens
+    # the region, step i's encode ends at event 2i+1 (1 + i without a decode)
+    # and its decode at 2i+2, which also starts step i+1's encode (each event
+    # record costs the stream ~5 us, so boundaries are not recorded twice)
+    per = 2 if dec is not None else 1
+
+    def step(i=None):
         enc.launch(stream.cuda_stream)
-        if ev is not None:
-            ev[1].record(stream)
+        if i is not None:
+            evs[per * i + 1].record(stream)
         if dec is not None:
             dec.launch(stream.cuda_stream)
-            if ev is not None:
-                ev[2].record(stream)
+            if i is not None:
+                evs[per * i + 2].record(stream)
 
     for _ in range(args.warmup):
         step()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(per * args.steps + 1)]
+    for e in evs:  # torch creates the HIP event at its first record: do that here, not in the timed loop
+        e.record(stream)
     torch.cuda.synchronize(dev)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
     barrier(world)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    evs[0].record(stream)
     for i in range(args.steps):
-        step(evs[i])
+        step(i)
     torch.cuda.synchronize(dev)
     # each rank's clock stops when its own GPU work has drained; the closing
     # barrier still brackets the region and the max over ranks below makes
@@ -570,10 +618,9 @@ def main(argv=None):
     barrier(world)
     t = max_over_ranks(elapsed, world)
 
-    enc_ms = median([e[0].elapsed_time(e[1]) for e in evs])
-    dec_ms = median([e[1].elapsed_time(e[2]) for e in evs]) if dec is not None else None
-    enc_bytes = (k + m) * S * B  # algorithmic HBM bytes per encode launch
-    dec_bytes = (k + len(erasures)) * S * B if erasures else 0  # k survivors read + erased shards written
+    enc_ms = median([evs[per * i].elapsed_time(evs[per * i + 1]) for i in range(args.steps)])
+    dec_ms = (median([evs[2 * i + 1].elapsed_time(evs[2 * i + 2]) for i in range(args.steps)]) if dec is not None
+              else None)
     user_per_stripe = (2 if erasures else 1) * k * S
     value = world * args.steps * B * user_per_stripe / t / 2**30
 
@@ -586,29 +633,44 @@ def main(argv=None):
     ref.launch(stream.cuda_stream)
     torch.cuda.synchronize(dev)
     ok = all(bool(torch.equal(chk[i], shards[0][k + i])) for i in range(m))
-    host_stripe = slab[0, :, :S].cpu().numpy() if (rank == 0 and world == 1 and args.cpu_seconds > 0) else None
+    # rank 0's stripe 0 for the CPU baseline (taken at every N: SURVEY.md §8d,
+    # the reference CPU path timed in the same run)
+    host_stripe = slab[0, :, :S].cpu().numpy() if (rank == 0 and args.cpu_seconds > 0) else None
 
-    per_rank = gather({"rank": rank, "device": local, "elapsed_s": round(elapsed, 6),
-                       "encode_median_ms": round(enc_ms, 4),
-                       "decode_median_ms": round(dec_ms, 4) if dec_ms is not None else None,
-                       "stripe_ids": [ids[0], ids[-1], len(ids)], "parity_ok": ok}, world)
-    ok = all(p["parity_ok"] for p in per_rank)
-
-    copy = None
+    enc_bytes = (k + m) * S * B  # algorithmic HBM bytes per encode launch
+    dec_bytes = (k + len(erasures)) * S * B if erasures else 0  # k survivors read + erased shards written
+    main_entries = {}
+    if not args.no_configs and args.config == "C3":
+        e = {"workload": f"RS(10,4) encode, 4 MiB shards, {B} stripes (the timed steps)"}
+        e.update(roofline_entry(enc_bytes, enc_ms))
+        main_entries["C3_encode"] = e
+        e = {"workload": f"RS(10,4) decode of erasure {{0}} (XOR-only), 4 MiB shards, {B} stripes (the timed steps)"}
+        e.update(roofline_entry(dec_bytes, dec_ms))
+        main_entries["C3_decode_0"] = e
+        main_entries.update(c3_decode_shapes(E, shards, S, B, dev, stream, kind, bool(args.nt)))
+    del enc, dec, ref
+    copy = copy_ceiling(slab, S)  # after the parity checks: the copy overwrites the slab's second half
     configs = None
-    if rank == 0:
-        copy = copy_ceiling(slab, S)  # after the parity checks: the copy overwrites the slab's second half
-        if world == 1 and not args.no_configs:
-            main_entries = {}
-            if args.config == "C3":
-                e = {"workload": f"RS(10,4) encode, 4 MiB shards, {B} stripes (the timed steps)"}
-                e.update(roofline_entry(enc_bytes, enc_ms))
-                main_entries["C3_encode"] = e
-                e = {"workload": f"RS(10,4) decode of erasure {{0}}, 4 MiB shards, {B} stripes (the timed steps)"}
-                e.update(roofline_entry(dec_bytes, dec_ms))
-                main_entries["C3_decode_0"] = e
-            del enc, dec, ref
-            configs = config_block(E, N, dev, stream, kind, bool(args.nt), main_entries)
+    if not args.no_configs:
+        del shards
+        slab = None
+        torch.cuda.empty_cache()
+        configs = config_block(E, N, dev, stream, kind, bool(args.nt), main_entries)
+
+    enc_frac = enc_bytes / (enc_ms / 1e3) / 1e9 / HBM_PEAK_GBS
+    mine = {"rank": rank, "device": local, "elapsed_s": round(elapsed, 6),
+            "encode_median_ms": round(enc_ms, 4), "encode_frac": round(enc_frac, 4),
+            "decode_median_ms": round(dec_ms, 4) if dec_ms is not None else None,
+            "decode_frac": (round(dec_bytes / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if dec_ms is not None
+                            else None),
+            "stripe_ids": [ids[0], ids[-1], len(ids)], "parity_ok": ok,
+            "copy_ceiling_GBps": copy["GBps"] if copy else None}
+    if configs:
+        mine["configs"] = {name: {"median_launch_ms": e["median_launch_ms"], "frac": e["frac"]}
+                           for name, e in configs.items()}
+    per_rank = gather(mine, world)
+    ok = all(p["parity_ok"] for p in per_rank)
+    barrier(world)  # every rank's GPU work is done: the CPU baseline below runs alone
 
     workload = C["workload"].format(B=B)
     cpu_ok = None
@@ -625,6 +687,10 @@ def main(argv=None):
                 cpu_ok = cpu_ok and ok_o3
         achieved = enc_bytes / (enc_ms / 1e3) / 1e9
         wkey = f"{args.config}:{B}"
+        kernel_id = N.lib.ecgpu_build_id(1).decode()
+        traffic, traffic_note = load_traffic("encode", wkey, kernel_id)
+        dec_traffic, dec_traffic_note = load_traffic("decode", wkey, kernel_id)
+        fracs = [p["encode_frac"] for p in per_rank]
         out = {
             "metric": C["metric"],
             "value": round(value, 3),
@@ -639,13 +705,14 @@ def main(argv=None):
             "dtype": "u8",
             "data": "synthetic (uniform random bytes, device-generated per global stripe id)",
             "config": {"workload": workload, "k": k, "m": m, "shard_bytes": S, "stripes_per_gpu": B,
-                       "shard_stride_bytes": int(slab.stride(1)),
+                       "shard_stride_bytes": shard_stride,
                        "erasures": erasures, "kernel": args.kernel, "nontemporal": bool(args.nt),
                        "parallelism": f"stripes round-robin over {world} GPU(s), no collective"},
             "rehearsal": rehearsal,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic("encode", wkey),
-                         "kernel": "gf_apply (encode launch)", "algorithmic_bytes_per_launch": enc_bytes,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_note,
+                         "frac_worst_rank": min(fracs), "frac_per_rank": fracs,
+                         "kernel": "gf_apply (encode launch, rank 0)", "algorithmic_bytes_per_launch": enc_bytes,
                          "median_launch_ms": round(enc_ms, 4), "kernel_time_stat": "median of HIP events",
                          # the north star's read-only accounting: data-shard bytes only, which
                          # caps at k/(k+m) of peak for any encode
@@ -655,7 +722,10 @@ def main(argv=None):
             "decode_kernel": ({"erasures": erasures, "median_launch_ms": round(dec_ms, 4),
                                "algorithmic_bytes_per_launch": dec_bytes,
                                "achieved_GBps": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),
-                               "traffic": load_traffic("decode", wkey)} if dec_ms is not None else None),
+                               "traffic": dec_traffic, "traffic_source": dec_traffic_note,
+                               "note": "decode{0} is XOR-only (parity 0 is the all-ones row); the decodes that "
+                                       "multiply are configs.C3_decode_parity and configs.C4_decode_0123"}
+                              if dec_ms is not None else None),
             "per_rank": per_rank,
             "configs": configs,
             "cpu_baseline": cpu,
@@ -663,6 +733,7 @@ def main(argv=None):
             "cpu_baseline_o3": cpu_o3,
             "selfcheck_parity_ok": ok,
             "selfcheck_vs_reference_cpu": cpu_ok,
+            "build_id": {"library": N.lib.ecgpu_build_id(0).decode(), "kernels": kernel_id},
         }
         print(json.dumps(out), flush=True)
     barrier(world)

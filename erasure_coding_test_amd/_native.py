@@ -38,6 +38,7 @@ KERNEL_PERM, KERNEL_LDS = 0, 1
 # that every declared symbol is exported).
 SIGNATURES = {
     "ecgpu_version": (c_char_p, []),
+    "ecgpu_build_id": (c_char_p, [c_int]),
     "ecgpu_last_error": (c_char_p, []),
     "ecgpu_free": (None, [c_void_p]),
     "ecgpu_galois_single_multiply": (c_int, [c_int, c_int, c_int]),

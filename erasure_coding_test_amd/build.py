@@ -1,6 +1,6 @@
 """In-tree build of the native libraries (gfx950 only).
 
-    python -m erasure_coding_test_amd.build          # or __graft_entry__.build()
+    python erasure_coding_test_amd/build.py          # or __graft_entry__.build()
 
 Produces, under erasure_coding_test_amd/lib/:
   libecgpu.so        -- the C ABI of include/ecgpu.h: HIP kernels (hipcc,
@@ -10,10 +10,19 @@ Produces, under erasure_coding_test_amd/lib/:
                         libecgpu.so (rpath $ORIGIN)
 and the test-only checker under oracle/ (make -C oracle).
 
-Objects are rebuilt only when a source is newer than its object.
+An object is rebuilt when its key changes: a SHA-256 of its compiler command
+line and the bytes of its source and every header (stored beside it as
+<object>.key), so neither a touched-but-unchanged file nor a stale object with
+a newer mtime decides.  The library carries two IDs (ecgpu_build_id):
+  0  the whole library: every source and header under csrc/ + ecgpu.h + flags
+  1  the coding kernels and their dispatch (gf_kernels / gf_spec / the runtime
+     and planner that pick grids, engines and cache policies) + HIP flags --
+     the identity a rocprofv3 PMC record of a launch is valid for
+     (profiles/summarize.py writes it, bench.py checks it).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -60,11 +69,54 @@ def _run_parallel(cmds):
             f.result()
 
 
-def _stale(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+KERNEL_ID_SRCS = ["gf_kernels.hpp", "gf_spec.hip", "gf_spec.hpp", "ecgpu_runtime.hip", "runtime.hpp", "planner.cpp",
+                  "planner.hpp"]
+
+
+def _digest(parts, files) -> str:
+    h = hashlib.sha256()
+    for p in parts:
+        h.update(p.encode())
+        h.update(b"\0")
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def build_ids() -> dict:
+    """{'build': ..., 'kernels': ...}: 16-hex content IDs (see module doc)."""
+    all_srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                      if f.endswith((".hip", ".cpp", ".hpp")) and f != "diag_kernels.hip")
+    return {"build": _digest([ARCH] + CXXFLAGS + HIPFLAGS, all_srcs + [os.path.join(INCLUDE, "ecgpu.h")])[:16],
+            "kernels": _digest([ARCH] + HIPFLAGS, [os.path.join(CSRC, f) for f in KERNEL_ID_SRCS])[:16]}
+
+
+def _stale(target, deps, cmd=()):
+    """True when `target` must be rebuilt; records the new key when so (the
+    caller builds it next; a failed build raises before anything reads it)."""
+    key = _digest(list(cmd), [d for d in deps if os.path.exists(d)])
+    stamp = target + ".key"
+    try:
+        with open(stamp) as f:
+            if os.path.exists(target) and f.read().strip() == key:
+                return False
+    except OSError:
+        pass
+    _pending_keys[stamp] = key
+    return True
+
+
+_pending_keys: dict = {}
+
+
+def _commit_keys():
+    for stamp, key in _pending_keys.items():
+        with open(stamp, "w") as f:
+            f.write(key + "\n")
+    _pending_keys.clear()
 
 
 def _headers():
@@ -75,44 +127,60 @@ def build_native(verbose: bool = True) -> dict:
     os.makedirs(LIB, exist_ok=True)
     os.makedirs(OBJ, exist_ok=True)
     hdrs = _headers()
+    ids = build_ids()
     objs = []
     for src in HOST_SRCS:
         s, o = os.path.join(CSRC, src), os.path.join(OBJ, src + ".o")
-        if _stale(o, [s] + hdrs):
-            _run([CXX] + CXXFLAGS + ["-fvisibility=hidden", "-c", s, "-o", o])
+        extra = ([f'-DECGPU_BUILD_ID="{ids["build"]}"', f'-DECGPU_KERNEL_ID="{ids["kernels"]}"']
+                 if src == "capi_host.cpp" else [])
+        cmd = [CXX] + CXXFLAGS + extra + ["-fvisibility=hidden", "-c", s, "-o", o]
+        if _stale(o, [s] + hdrs, cmd):
+            _run(cmd)
         objs.append(o)
     jobs = []
     for src, obj, extra in HIP_UNITS:
         s, o = os.path.join(CSRC, src), os.path.join(OBJ, obj)
-        if _stale(o, [s] + hdrs):
-            jobs.append([HIPCC] + HIPFLAGS + extra + ["-c", s, "-o", o])
+        cmd = [HIPCC] + HIPFLAGS + extra + ["-c", s, "-o", o]
+        if _stale(o, [s] + hdrs, cmd):
+            jobs.append(cmd)
         objs.append(o)
     _run_parallel(jobs)
+    _commit_keys()
     ecgpu = os.path.join(LIB, "libecgpu.so")
-    if _stale(ecgpu, objs):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,-soname,libecgpu.so"] + objs + ["-o", ecgpu])
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,-soname,libecgpu.so"] + objs + ["-o", ecgpu]
+    if _stale(ecgpu, objs, cmd):
+        _run(cmd)
+        _commit_keys()
 
     dropin_objs = []
     for src in DROPIN_SRCS:
         s, o = os.path.join(CSRC, src), os.path.join(OBJ, src + ".o")
-        if _stale(o, [s] + hdrs + [os.path.join(INCLUDE, "dropin", h) for h in ("galois.h", "jerasure.h", "reed_sol.h")]):
-            _run([CXX] + CXXFLAGS + [f"-I{os.path.join(INCLUDE, 'dropin')}", "-fvisibility=hidden",
-                                     "-fvisibility-inlines-hidden", "-c", s, "-o", o])
+        cmd = [CXX] + CXXFLAGS + [f"-I{os.path.join(INCLUDE, 'dropin')}", "-fvisibility=hidden",
+                                  "-fvisibility-inlines-hidden", "-c", s, "-o", o]
+        if _stale(o, [s] + hdrs + [os.path.join(INCLUDE, "dropin", h) for h in ("galois.h", "jerasure.h", "reed_sol.h")],
+                  cmd):
+            _run(cmd)
+            _commit_keys()
         dropin_objs.append(o)
     # the CPU-surface code reuses the host GF / matrix objects (hidden symbols)
     dropin_objs += [os.path.join(OBJ, s + ".o") for s in ("gf_host.cpp", "matrix_host.cpp", "schedule_host.cpp")]
     dropin = os.path.join(LIB, "libjerasure_amd.so")
-    if _stale(dropin, dropin_objs + [ecgpu]):
-        _run([CXX, "-shared", "-fPIC"] + dropin_objs +
-             ["-o", dropin, f"-L{LIB}", "-lecgpu", "-Wl,-rpath,$ORIGIN"])
-    out = {"libecgpu": ecgpu, "libjerasure_amd": dropin}
+    cmd = [CXX, "-shared", "-fPIC"] + dropin_objs + ["-o", dropin, f"-L{LIB}", "-lecgpu", "-Wl,-rpath,$ORIGIN"]
+    if _stale(dropin, dropin_objs + [ecgpu], cmd):
+        _run(cmd)
+        _commit_keys()
+    out = {"libecgpu": ecgpu, "libjerasure_amd": dropin, "build_ids": ids}
     if os.environ.get("ECGPU_BUILD_DIAG", "1") != "0":
         s, o = os.path.join(CSRC, "diag_kernels.hip"), os.path.join(OBJ, "diag_kernels.hip.o")
         diag = os.path.join(LIB, "libecgpu_diag.so")
-        if _stale(o, [s] + hdrs):
-            _run([HIPCC] + HIPFLAGS + ["-c", s, "-o", o])
-        if _stale(diag, [o]):
-            _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", o, "-o", diag])
+        cmd = [HIPCC] + HIPFLAGS + ["-c", s, "-o", o]
+        if _stale(o, [s] + hdrs, cmd):
+            _run(cmd)
+            _commit_keys()
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", o, "-o", diag]
+        if _stale(diag, [o], cmd):
+            _run(cmd)
+            _commit_keys()
         out["libecgpu_diag"] = diag
     return out
 

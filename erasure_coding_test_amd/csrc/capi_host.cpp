@@ -14,6 +14,16 @@ using namespace ecgpu;
 extern "C" {
 
 ECGPU_API const char* ecgpu_version(void) { return "ecgpu 0.1 (gfx950)"; }
+
+// Content IDs of this build (erasure_coding_test_amd/build.py): 0 the whole
+// library, 1 the coding kernels and their dispatch.
+#ifndef ECGPU_BUILD_ID
+#define ECGPU_BUILD_ID "unknown"
+#endif
+#ifndef ECGPU_KERNEL_ID
+#define ECGPU_KERNEL_ID "unknown"
+#endif
+ECGPU_API const char* ecgpu_build_id(int what) { return what == 1 ? ECGPU_KERNEL_ID : ECGPU_BUILD_ID; }
 ECGPU_API void ecgpu_free(void* p) { std::free(p); }
 
 constexpr int64_t kShardSkew = 10240;

@@ -53,6 +53,10 @@ enum { ECGPU_KERNEL_PERM = 0, ECGPU_KERNEL_LDS = 1 };
 
 /* ---------------------------------------------------------------- misc -- */
 ECGPU_API const char* ecgpu_version(void);
+/* Content IDs of the built library (16 hex digits): what = 0 the whole
+ * library, 1 the coding kernels and their dispatch (the identity a rocprofv3
+ * PMC record of a launch is valid for). */
+ECGPU_API const char* ecgpu_build_id(int what);
 ECGPU_API const char* ecgpu_last_error(void);         /* thread-local message */
 ECGPU_API void ecgpu_free(void* p);                    /* == free()           */
 

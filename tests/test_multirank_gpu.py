@@ -146,9 +146,13 @@ def _line(out):
     return json.loads(lines[0])
 
 
+@pytest.mark.timeout(420)
 def test_bench_gpus2_rehearsal_spawns_two_ranks(gpu):
-    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--stripes", "4", "--cpu-seconds", "0",
-                "--no-configs"], {"ECGPU_BENCH_ONE_DEVICE": "1"})
+    # the N > 1 line is complete: rank 0's CPU baseline on
+    # its stripe 0, every rank's encode / decode fractions and configs block
+    # (incl. C4), the worst-rank roofline fraction beside rank 0's
+    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--stripes", "4", "--cpu-seconds", "1"],
+               {"ECGPU_BENCH_ONE_DEVICE": "1"}, timeout=400)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and d["rehearsal"] is True
@@ -156,6 +160,17 @@ def test_bench_gpus2_rehearsal_spawns_two_ranks(gpu):
     assert all(p["parity_ok"] for p in d["per_rank"])
     assert [p["stripe_ids"] for p in d["per_rank"]] == [[0, 6, 4], [1, 7, 4]]  # round-robin global ids
     assert d["selfcheck_parity_ok"] is True
+    roof = d["roofline"]
+    assert roof["frac"] > 0 and len(roof["frac_per_rank"]) == 2
+    assert roof["frac_worst_rank"] == min(roof["frac_per_rank"])
+    assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] == 1
+    assert d["selfcheck_vs_reference_cpu"] is True
+    for p in d["per_rank"]:
+        assert p["encode_frac"] > 0 and p["decode_frac"] > 0
+        assert {"C2_encode", "C3_encode", "C3_decode_0", "C3_decode_parity", "C3_decode_data_random",
+                "C4_decode_0123", "C5_encode"} <= set(p["configs"])
+        assert p["configs"]["C4_decode_0123"]["frac"] > 0
+    assert d["configs"]["C3_decode_parity"]["algorithmic_bytes_per_launch"] == 11 * (4 << 20) * 4
 
 
 def test_bench_gpus_beyond_visible_devices_fails(gpu):

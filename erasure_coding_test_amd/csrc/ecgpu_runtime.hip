@@ -430,8 +430,13 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
     const int R = std::min(dev::kMaxRows, p->rows - r0);
     // w = 16 packs two rows per LDS dword (gf_apply_wide_nib16, half the LDS bytes)
     const bool pack16 = W == 2 && env_int("ECGPU_NIB16", 1) != 0;
-    const unsigned nib_lds =
-        unsigned(K) * unsigned(pack16 ? dev::nib16_source_bytes(R) : dev::nib_source_bytes(R));
+    // the 32-bit-entry kernel's unit structure (gf_apply_wide_nib<R, 1>): the
+    // launch's row 0 and column 0 all ones, as in every Vandermonde encode
+    bool unit_rc = !pack16 && R >= 2 && env_int("ECGPU_WIDE_UNITS", 1) != 0;
+    for (int j = 0; j < K && unit_rc; ++j) unit_rc = p->coef[size_t(r0) * K + j] == 1u;
+    for (int r = 0; r < R && unit_rc; ++r) unit_rc = p->coef[size_t(r0 + r) * K] == 1u;
+    const unsigned nib_lds = pack16 ? unsigned(K) * unsigned(dev::nib16_source_bytes(R))
+                                    : unsigned(dev::nib_lds_bytes(K, R, unit_rc ? 1 : 0));
     const bool nib = !force_perm && nib_lds <= unsigned(dev::kNibMaxLds);
     KernelFn vec_fn = nullptr, word_fn = W == 2 ? &dev::gf_apply_wide_words<2> : &dev::gf_apply_wide_words<4>;
     if (nib && pack16) {
@@ -440,6 +445,12 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
         case 2: vec_fn = &dev::gf_apply_wide_nib16<2>; break;
         case 3: vec_fn = &dev::gf_apply_wide_nib16<3>; break;
         default: vec_fn = &dev::gf_apply_wide_nib16<4>; break;
+      }
+    } else if (nib && unit_rc) {
+      switch (R) {
+        case 2: vec_fn = &dev::gf_apply_wide_nib<2, 1>; break;
+        case 3: vec_fn = &dev::gf_apply_wide_nib<3, 1>; break;
+        default: vec_fn = &dev::gf_apply_wide_nib<4, 1>; break;
       }
     } else if (nib) {
       switch (R) {
@@ -876,7 +887,9 @@ int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, cons
   const int64_t nbb = (size - byte0 + dev::kBlock - 1) / dev::kBlock;
   for (int r0 = 0; r0 < rows; r0 += dev::kMaxRows) {
     const int R = std::min(dev::kMaxRows, rows - r0);
-    const InlineKernelFn fn = inline_kernel(K, R, unit_variant(op.coef, K, r0, R));
+    // the grid-stride form only where the grid is capped (host memory in place)
+    const bool zc = nbv * dev::kBlock < nvec;
+    const InlineKernelFn fn = inline_kernel(K, R, unit_variant(op.coef, K, r0, R), zc);
     if (!fn) return fail(ECGPU_ERR, "no inline kernel for K = " + std::to_string(K));
     dev::InlineArgs a{};
     for (int j = 0; j < K; ++j) a.src[j] = sp[size_t(j)];
@@ -885,11 +898,21 @@ int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, cons
     a.size = size;
     a.byte0 = byte0;
     a.nblk_vec = int(nbv);
+    int mul_terms = 0;  // coefficients that are neither 0 nor 1
     for (int r = 0; r < R; ++r)
-      for (int j = 0; j < K; ++j) build_p3(op.coef[size_t(r0 + r) * K + j], &a.ptab[(r * K + j) * dev::kP3Words]);
+      for (int j = 0; j < K; ++j) {
+        const uint32_t c = op.coef[size_t(r0 + r) * K + j];
+        build_p3(c, &a.ptab[(r * K + j) * dev::kP3Words]);
+        mul_terms += c > 1u;
+      }
+    // device buffers: the plan launches' residency cap (cap_for) -- a large
+    // one-stripe call streams K + R shards per lane like a batched launch
+    // (RS(10,4) 64 MiB encode, separately allocated shards: 275 us uncapped)
+    const unsigned lds =
+        !host_io && nvec > 0 && cap_for(K, R, mul_terms) ? residency_lds_bytes(current_device(), K + R) : 0u;
     void* args[] = {&a};
     ECGPU_HIP(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(unsigned(nbv + nbb)), dim3(dev::kBlock), args,
-                              0, s));
+                              lds, s));
   }
   return ECGPU_OK;
 }

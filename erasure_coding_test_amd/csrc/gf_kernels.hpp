@@ -98,6 +98,19 @@ __device__ __forceinline__ u32x4 load16t(const uint8_t* p, int64_t col) {
   else return *a;
 }
 
+// A kernel-invariant table entry (pointer tables, row masks) read through the
+// constant address space: always a scalar load.  A generic load issued after
+// the kernel's own vector stores must be a VECTOR load (the scalar cache is
+// not coherent with vector stores), and waiting for it (vmcnt(0)) waits for
+// every shard load issued before it -- in a column loop that serialised the
+// K source loads of each iteration.  Valid because no table is written while
+// a kernel runs.
+template <class T>
+__device__ __forceinline__ T kload(const T* p, int64_t i) {
+  typedef __attribute__((address_space(4))) const T kT;
+  return ((const kT*)p)[i];  // C cast: generic -> constant
+}
+
 // Store cache policy POL: 0 plain, 1 non-temporal (`nt`).  (Stores that
 // bypass the XCD's L2 -- `sc1`, `sc0 sc1`, inline asm -- were probed in round
 // 1 and were equal or slower in the bench's back-to-back launches, DESIGN.md
@@ -473,23 +486,42 @@ struct InlineArgs {
 static_assert(sizeof(InlineArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 
 template <int K, int R, int UNITS>
+__device__ __forceinline__ void inl_column(const uint8_t* const (&sp)[K], uint8_t* const (&dp)[R],
+                                           const kconst_u32* t, int64_t col) {
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = load16t<1>(sp[j], col);
+  u32x4 acc[R];
+  combine3<K, R, UNITS>(t, x, acc);
+#pragma unroll
+  for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
+}
+
+// ZC = false (device buffers): one 16-B column per lane, straight-line like
+// gf_apply -- in a loop the compiler hoists every table load out of it,
+// which overflows the SGPR file into VGPR lanes (RS(10,4): 180 v_readlane,
+// 132 VGPRs; a 64 MiB encode took 271 us against gf_apply's 157).
+// ZC = true (host memory read and written in place over PCIe): grid-stride
+// over a capped grid -- fewer PCIe requests in flight read faster
+// (tools/zero_copy_probe.cpp); PCIe-bound, so the spills do not matter there.
+template <int K, int R, int UNITS, bool ZC>
 __global__ __launch_bounds__(kBlock) void gf_apply_inl(InlineArgs a) {
   const kconst_u32* ptab = (const kconst_u32*)a.ptab;  // kernarg segment: scalar loads
   if (int(blockIdx.x) < a.nblk_vec) {
-    // grid-stride: a launch over host memory (zero-copy) runs a capped grid,
-    // fewer PCIe requests in flight read faster (tools/zero_copy_probe.cpp)
+    // (pointers copied out by value: a reference to the kernarg struct would
+    // copy all 2.2 KiB of it to scratch)
+    const uint8_t* sp[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sp[j] = a.src[j];
     uint8_t* dp[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) dp[r] = a.dst[r];
-    const int64_t step = int64_t(a.nblk_vec) * kBlock;
-    for (int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x; col < a.nvec; col += step) {
-      u32x4 x[K];
-#pragma unroll
-      for (int j = 0; j < K; ++j) x[j] = load16t<1>(a.src[j], col);
-      u32x4 acc[R];
-      combine3<K, R, UNITS>(ptab, x, acc);
-#pragma unroll
-      for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
+    int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if constexpr (!ZC) {
+      if (col < a.nvec) inl_column<K, R, UNITS>(sp, dp, ptab, col);
+    } else {
+      const int64_t step = int64_t(a.nblk_vec) * kBlock;
+      for (; col < a.nvec; col += step) inl_column<K, R, UNITS>(sp, dp, ptab, col);
     }
     return;
   }
@@ -1057,16 +1089,16 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets16(PacketArgs a) {
   for (; j + CHUNK <= a.nsrc; j += CHUNK) {
     u32x4 x[CHUNK];
 #pragma unroll
-    for (int u = 0; u < CHUNK; ++u) x[u] = load16t<1>(a.src[j + u] + soff, 0);
+    for (int u = 0; u < CHUNK; ++u) x[u] = load16t<1>(kload(a.src, j + u) + soff, 0);
 #pragma unroll
-    for (int u = 0; u < CHUNK; ++u) xor_masked16<RT, CHUNK>(acc, x[u], a.mask[j + u]);
+    for (int u = 0; u < CHUNK; ++u) xor_masked16<RT, CHUNK>(acc, x[u], kload(a.mask, j + u));
   }
-  for (; j < a.nsrc; ++j) xor_masked16<RT, CHUNK>(acc, load16t<1>(a.src[j] + soff, 0), a.mask[j]);
+  for (; j < a.nsrc; ++j) xor_masked16<RT, CHUNK>(acc, load16t<1>(kload(a.src, j) + soff, 0), kload(a.mask, j));
   // output pointers only now: held across the loop they would take RT SGPR
-  // pairs from the row selectors (no store precedes these scalar loads)
+  // pairs from the row selectors (kload: scalar loads between the stores)
 #pragma unroll
   for (int r = 0; r < RT; ++r)
-    if (r < a.R) store16t<1>(a.dst[r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+    if (r < a.R) store16t<1>(kload(a.dst, r) + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
 }
 
 // Production 16-B form (packets, strides and bases 16-B aligned): source
@@ -1093,8 +1125,8 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets16p(PacketArgs a) {
     const int b = (c < nc ? c : nc - 1) * 4;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      m[u] = a.mask[b + u];
-      x[u] = load16t<1>(a.src[b + u] + soff, 0);
+      m[u] = kload(a.mask, b + u);
+      x[u] = load16t<1>(kload(a.src, b + u) + soff, 0);
     }
   };
   auto apply4 = [&](const u32x4 (&x)[4], const uint32_t (&m)[4]) {
@@ -1111,10 +1143,10 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets16p(PacketArgs a) {
       apply4(xb, mb);
     }
   }
-  for (int j = nc * 4; j < a.nsrc; ++j) xor_masked16<RT, 4>(acc, load16t<1>(a.src[j] + soff, 0), a.mask[j]);
+  for (int j = nc * 4; j < a.nsrc; ++j) xor_masked16<RT, 4>(acc, load16t<1>(kload(a.src, j) + soff, 0), kload(a.mask, j));
 #pragma unroll
   for (int r = 0; r < RT; ++r)
-    if (r < a.R) store16t<1>(a.dst[r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+    if (r < a.R) store16t<1>(kload(a.dst, r) + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
 }
 
 // Byte form for packet sizes / bases that are not 8-byte aligned.
@@ -1160,20 +1192,39 @@ constexpr int kNibMaxLds = 64 * 1024;
 __host__ __device__ constexpr int nib_entry_words(int R) { return R <= 2 ? 2 : 4; }
 // LDS bytes of one source's tables for a launch of R rows
 __host__ __device__ constexpr int nib_source_bytes(int R) { return kNibWords * 4 * nib_entry_words(R); }
+// ... and of the whole launch: U = 1 (row 0 and column 0 all ones, below)
+// keeps rows 1..R-1 of sources 1..K-1 only
+__host__ __device__ constexpr int nib_lds_bytes(int K, int R, int U) {
+  return (K - U) * nib_source_bytes(R - U);
+}
 
 typedef __attribute__((address_space(3))) const u32x2 lds_u32x2;
 
-template <int R>
+// U = 1: the launch's row 0 and column 0 are all ones -- every
+// reed_sol_vandermonde_coding_matrix encode (reed_sol.cpp:324-349), checked
+// exactly by the host per launch.  Row 0 is then the XOR of the sources and
+// source 0 is XORed into every row: no lookups for either, and the LDS holds
+// the L = R - 1 other rows of sources 1..K-1 (RS(10,4) w = 32: 72 instead of
+// 80 ds_read_b128 per lane-column).  With fewer registers live (four source
+// loads in flight, the eight lookups folded in two groups of four) the kernel
+// runs 7 waves per SIMD instead of 5 (68 VGPRs).  RS(10,4) w = 32 64 MiB,
+// tools/wide_lab.hip, 15 interleaved rounds: 191-195 us against 204-209 for
+// the U = 0 form (profiles/r03_wide_lab.jsonl).
+template <int R, int U = 0>
 __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib(ApplyArgs a) {
-  constexpr int EW = nib_entry_words(R), EB = 4 * EW;
+  static_assert(U == 0 || R >= 2, "U = 1 needs a row besides the unit row");
+  constexpr int L = R - U;  // rows looked up in LDS
+  constexpr int EW = nib_entry_words(L), EB = 4 * EW;
+  constexpr int kChunk = U ? 4 : 8;   // source loads in flight before the first use
+  constexpr int kGroups = U ? 2 : 1;  // lookups issued and folded in kGroups groups
   extern __shared__ __attribute__((aligned(16))) uint8_t nib_lds[];
   const int K = a.K;
-  // LDS dword ((j * 128 + t * 16 + v) * EW + r) = T[r][j][t][v] (0 for r >= R);
+  // LDS dword (((j - U) * 128 + t * 16 + v) * EW + l) = T[l + U][j][t][v] (0 for l >= L);
   // a.wtab is [R][K][kNibWords] for this launch's rows
-  const int n = K * kNibWords * EW;
+  const int n = (K - U) * kNibWords * EW;
   for (int i = threadIdx.x; i < n; i += kBlock) {
-    const int r = i % EW, e = (i / EW) % kNibWords, j = i / (EW * kNibWords);
-    reinterpret_cast<uint32_t*>(nib_lds)[i] = r < R ? a.wtab[size_t(r * K + j) * kNibWords + e] : 0u;
+    const int l = i % EW, e = (i / EW) % kNibWords, j = i / (EW * kNibWords) + U;
+    reinterpret_cast<uint32_t*>(nib_lds)[i] = l < L ? a.wtab[size_t((l + U) * K + j) * kNibWords + e] : 0u;
   }
   __syncthreads();
 
@@ -1183,7 +1234,6 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib(ApplyArgs a) {
 #pragma unroll
   for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
   const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(static_cast<void*>(nib_lds)));
-  constexpr int kChunk = 8;  // source loads in flight before the first use
   const int64_t nblk = (a.nvec + kBlock - 1) / kBlock;
   for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
     const int64_t col = b * kBlock + threadIdx.x;
@@ -1195,14 +1245,22 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib(ApplyArgs a) {
       u32x4 xs[kChunk];
 #pragma unroll
       for (int u = 0; u < kChunk; ++u)
-        if (j0 + u < K) xs[u] = load16t<1>(sp[j0 + u], col);
+        if (j0 + u < K) xs[u] = load16t<1>(kload(sp, j0 + u), col);
 #pragma unroll
       for (int u = 0; u < kChunk; ++u) {
         const int j = j0 + u;
         if (j >= K) break;
+        if (U == 1) {
+          if (j == 0) {  // column 0: a unit in every row
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] ^= xs[u];
+            continue;
+          }
+          acc[0] ^= xs[u];  // row 0: units
+        }
         // LDS byte address of source j's tables; the kernel has no static LDS,
         // so the dynamic allocation starts at 0 and jbase < 64 KiB (K <= 32)
-        const uint32_t jbase = lds_base + uint32_t(j) * uint32_t(nib_source_bytes(R));
+        const uint32_t jbase = lds_base + uint32_t(j - U) * uint32_t(nib_source_bytes(L));
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const uint32_t x = xs[u][c];
@@ -1213,27 +1271,32 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib(ApplyArgs a) {
           constexpr int kSh = EB == 16 ? 4 : 3;
           constexpr uint32_t kNibMask = 0x0F0F0F0Fu << kSh;
           const uint32_t ns[2] = {(x << kSh) & kNibMask, (x >> (4 - kSh)) & kNibMask};
-          uint32_t v[8][EW];
 #pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
-                                uint32_t(t * 16 * EB);
-            if constexpr (EW == 2) {
-              const u32x2 q = *(lds_u32x2*)(size_t(ad));
-              v[t][0] = q.x;
-              v[t][1] = q.y;
-            } else {
-              const u32x4 q = *(lds_u32x4*)(size_t(ad));
+          for (int g = 0; g < kGroups; ++g) {
+            constexpr int TN = 8 / kGroups;
+            uint32_t v[TN][EW];
 #pragma unroll
-              for (int r = 0; r < 4; ++r) v[t][r] = q[r];
+            for (int tt = 0; tt < TN; ++tt) {
+              const int t = g * TN + tt;
+              const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
+                                  uint32_t(t * 16 * EB);
+              if constexpr (EW == 2) {
+                const u32x2 q = *(lds_u32x2*)(size_t(ad));
+                v[tt][0] = q.x;
+                v[tt][1] = q.y;
+              } else {
+                const u32x4 q = *(lds_u32x4*)(size_t(ad));
+#pragma unroll
+                for (int l = 0; l < 4; ++l) v[tt][l] = q[l];
+              }
             }
-          }
 #pragma unroll
-          for (int r = 0; r < R; ++r) {
-            uint32_t e = xor3(acc[r][c], v[0][r], v[1][r]);
+            for (int l = 0; l < L; ++l) {
+              uint32_t e = acc[l + U][c];
 #pragma unroll
-            for (int t = 2; t < 8; t += 2) e = xor3(e, v[t][r], v[t + 1][r]);
-            acc[r][c] = e;
+              for (int tt = 0; tt < TN; tt += 2) e = xor3(e, v[tt][l], v[tt + 1][l]);
+              acc[l + U][c] = e;
+            }
           }
         }
       }
@@ -1295,7 +1358,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
       u32x4 xs[kChunk];
 #pragma unroll
       for (int u = 0; u < kChunk; ++u)
-        if (j0 + u < K) xs[u] = load16t<1>(sp[j0 + u], col);
+        if (j0 + u < K) xs[u] = load16t<1>(kload(sp, j0 + u), col);
 #pragma unroll
       for (int u = 0; u < kChunk; ++u) {
         const int j = j0 + u;

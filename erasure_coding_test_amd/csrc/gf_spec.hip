@@ -26,13 +26,14 @@ struct Pol {
                                             apply_fn<K, 3, S>(), apply_fn<K, 4, S>()};
 };
 
-template <int K, int U>
-constexpr InlineKernelFn inl_fn() { return &dev::gf_apply_inl<K, kR, kUnitVariants[U]>; }
+template <int K, int U, bool ZC>
+constexpr InlineKernelFn inl_fn() { return &dev::gf_apply_inl<K, kR, kUnitVariants[U], ZC>; }
 
 template <int K>
 struct Row {
-  static constexpr InlineKernelFn inl[5] = {inl_fn<K, 0>(), inl_fn<K, 1>(), inl_fn<K, 2>(), inl_fn<K, 3>(),
-                                            inl_fn<K, 4>()};
+  static constexpr InlineKernelFn inl[2][5] = {
+      {inl_fn<K, 0, false>(), inl_fn<K, 1, false>(), inl_fn<K, 2, false>(), inl_fn<K, 3, false>(), inl_fn<K, 4, false>()},
+      {inl_fn<K, 0, true>(), inl_fn<K, 1, true>(), inl_fn<K, 2, true>(), inl_fn<K, 3, true>(), inl_fn<K, 4, true>()}};
   static constexpr const SpecKernelFn* apply[kStorePolicies] = {Pol<K, 0>::apply, Pol<K, 1>::apply};
   static constexpr SpecKernelFn lds = &dev::gf_apply_lds<K, kR>;
 };
@@ -45,9 +46,9 @@ SpecKernelFn pick(bool lds, int K, int u, int store_pol) {
 }
 
 template <int... Ks>
-InlineKernelFn pick_inl(int K, int u) {
+InlineKernelFn pick_inl(int K, int u, bool zc) {
   InlineKernelFn out = nullptr;
-  ((K == Ks ? (out = Row<Ks>::inl[u], 0) : 0), ...);
+  ((K == Ks ? (out = Row<Ks>::inl[zc ? 1 : 0][u], 0) : 0), ...);
   return out;
 }
 
@@ -60,9 +61,9 @@ SpecKernelFn ECGPU_CAT(spec_kernel_r, ECGPU_SPEC_R)(bool lds, int K, int unit_va
   return pick<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>(lds, K, unit_variant, store_pol);
 }
 
-InlineKernelFn ECGPU_CAT(inline_kernel_r, ECGPU_SPEC_R)(int K, int unit_variant) {
+InlineKernelFn ECGPU_CAT(inline_kernel_r, ECGPU_SPEC_R)(int K, int unit_variant, bool zc) {
   if (unit_variant < 0 || unit_variant > 4) return nullptr;
-  return pick_inl<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>(K, unit_variant);
+  return pick_inl<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>(K, unit_variant, zc);
 }
 
 }  // namespace ecgpu

@@ -22,19 +22,20 @@ SpecKernelFn spec_kernel_r2(bool lds, int K, int unit_variant, int store_pol);
 SpecKernelFn spec_kernel_r3(bool lds, int K, int unit_variant, int store_pol);
 SpecKernelFn spec_kernel_r4(bool lds, int K, int unit_variant, int store_pol);
 
-// gf_apply_inl<K, R, UNITS> (one stripe, everything in the kernel
-// arguments); nullptr if K is outside 1..kMaxSpecK.
-InlineKernelFn inline_kernel_r1(int K, int unit_variant);
-InlineKernelFn inline_kernel_r2(int K, int unit_variant);
-InlineKernelFn inline_kernel_r3(int K, int unit_variant);
-InlineKernelFn inline_kernel_r4(int K, int unit_variant);
+// gf_apply_inl<K, R, UNITS, ZC> (one stripe, everything in the kernel
+// arguments; zc: the grid-stride form for host memory used in place);
+// nullptr if K is outside 1..kMaxSpecK.
+InlineKernelFn inline_kernel_r1(int K, int unit_variant, bool zc);
+InlineKernelFn inline_kernel_r2(int K, int unit_variant, bool zc);
+InlineKernelFn inline_kernel_r3(int K, int unit_variant, bool zc);
+InlineKernelFn inline_kernel_r4(int K, int unit_variant, bool zc);
 
-inline InlineKernelFn inline_kernel(int K, int R, int unit_variant) {
+inline InlineKernelFn inline_kernel(int K, int R, int unit_variant, bool zc) {
   switch (R) {
-    case 1: return inline_kernel_r1(K, unit_variant);
-    case 2: return inline_kernel_r2(K, unit_variant);
-    case 3: return inline_kernel_r3(K, unit_variant);
-    case 4: return inline_kernel_r4(K, unit_variant);
+    case 1: return inline_kernel_r1(K, unit_variant, zc);
+    case 2: return inline_kernel_r2(K, unit_variant, zc);
+    case 3: return inline_kernel_r3(K, unit_variant, zc);
+    case 4: return inline_kernel_r4(K, unit_variant, zc);
     default: return nullptr;
   }
 }

@@ -966,6 +966,43 @@ def test_wide_word_random_matrix_engines(ec, gpu, monkeypatch, w, engine, k, m):
         assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
 
 
+@pytest.mark.parametrize("w,nib16", [(32, "1"), (16, "0")])
+@pytest.mark.parametrize("units", ["1", "0"])
+@pytest.mark.parametrize("k,m", [(10, 4), (6, 2), (5, 3), (32, 4), (12, 6), (2, 2)])
+def test_wide_word_unit_structured_launches(ec, gpu, monkeypatch, w, nib16, units, k, m):
+    """Launches whose row 0 and column 0 are all ones (every Vandermonde
+    encode) run gf_apply_wide_nib<R, 1>: row 0 and source 0 by XOR, the other
+    rows of sources 1..K-1 from LDS (R = 2, 3, 4; m = 6 is a unit launch of
+    rows 0-3 plus a general launch of rows 4-5).  Random general coefficients
+    with zeros and units mixed in, against the reference library, with the
+    unit form on and off (ECGPU_WIDE_UNITS)."""
+    import torch
+    monkeypatch.delenv("ECGPU_WIDE", raising=False)
+    monkeypatch.setenv("ECGPU_NIB16", nib16)
+    monkeypatch.setenv("ECGPU_WIDE_UNITS", units)
+    ref = _ref_nsa()
+    rng = np.random.default_rng(77 * w + 10 * k + m)
+    hi = (1 << w) - 1
+    M = [int(x) for x in rng.integers(2, hi, k * m, dtype=np.uint64, endpoint=True)]
+    for i in rng.choice(k * m, size=(k * m) // 5, replace=False):
+        M[int(i)] = int(rng.integers(0, 2))
+    for j in range(k):
+        M[j] = 1  # row 0
+    for i in range(m):
+        M[i * k] = 1  # column 0
+    Mi = [x if x < 2**31 else x - 2**32 for x in M]
+    size = (1 << 18) + 32 + (w // 8)
+    data = [rng.integers(0, 256, size + 64, dtype=np.uint8) for _ in range(k)]
+    coding = [np.zeros(size + 64, np.uint8) for _ in range(m)]
+    ref._Z22jerasure_matrix_encodeiiiPiPPcS1_i(k, m, w, _cints(Mi), _cptrs(data), _cptrs(coding), size)
+    dd = [torch.from_numpy(a[:size].copy()).to(gpu) for a in data]
+    dc = [torch.full((size,), 0x5A, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, w, Mi, dd, dc, size)
+    torch.cuda.synchronize()
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
+
+
 @pytest.mark.parametrize("w", [16, 32])
 def test_wide_word_region_ops_device(ec, gpu, w):
     import torch

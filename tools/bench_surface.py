@@ -60,6 +60,15 @@ def main():
                 lambda M=M, w=w: J.jerasure_matrix_encode(k, m, w, M, data, coding, S))
             del os.environ["ECGPU_WIDE"]
     M8 = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    # the same shards through the batched plan API (gf_apply, pointer and
+    # coefficient tables in HBM) against the synchronous call's inline launch
+    plan = E.encode_plan(k, m, M8).bind([data], [coding], S)
+    rec("encode_plan w=8 (plan launch, same shards)", lambda: plan.launch())
+    # and on a skewed slab (the library's recommended shard stride)
+    slab, shards = E.alloc_stripes(1, k, m, S)
+    shards[0][0].copy_(data[0])
+    rec("jerasure_matrix_encode w=8, skewed slab",
+        lambda: J.jerasure_matrix_encode(k, m, 8, M8, shards[0][:k], shards[0][k:], S))
     bm = J.jerasure_matrix_to_bitmatrix(k, m, 8, M8)
     for ps in (1024, 4096, 65536):
         rec(f"jerasure_bitmatrix_encode w=8 packetsize={ps}",

@@ -1,0 +1,360 @@
+// wide_lab.hip -- A/B lab for the w = 32 (and w = 16) LDS nibble-table
+// column kernels: RS(k,m) encode of one stripe of S-byte device shards laid
+// out at the library's skewed stride, every variant checked bit-exact against
+// the production kernel (and that one against a host GF(2^w) multiply on
+// sample columns), then timed in interleaved rounds with HIP events.
+//
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I erasure_coding_test_amd/csrc \
+//     tools/wide_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp -o tools/wide_lab.bin
+//   tools/wide_lab.bin [--w 32] [--k 10] [--m 4] [--mib 64] [--rounds 7] [--reps 10] [--only name]
+//
+// Prints one JSON line per variant: median / min us and GB/s of (k+m)*S.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "gf_host.hpp"
+#include "gf_kernels.hpp"
+#include "matrix_host.hpp"
+
+using namespace ecgpu;
+using namespace ecgpu::dev;
+
+#define CK(x)                                                                            \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(1);                                                                      \
+    }                                                                                    \
+  } while (0)
+
+namespace lab {
+
+typedef __attribute__((address_space(3))) const uint32_t lds_u32c;
+typedef __attribute__((address_space(3))) const u32x2 lds_u32x2c;
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4c;
+typedef const uint8_t* gptr;
+typedef __attribute__((address_space(4))) const gptr kptr;  // a pointer-table entry in constant memory
+
+// Split-entry nibble kernel.  U = 1: row 0 and column 0 of the launch are all
+// ones (a Vandermonde encode), so row 0 is the XOR of the sources, source 0
+// is XORed into every row, and the LDS holds rows 1..R-1 of sources 1..K-1
+// only.  The L = R - U LDS rows are stored as NP = ceil(L/2) pair tables of
+// 8-B entries per (source, nibble t) (the last one a single row read with
+// ds_read_b32 when L is odd), or, with B128 and L = 4, one 16-B entry.
+template <int R, int U, bool B128, int CHUNK = 8, int HALVES = 1, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void nib_split(ApplyArgs a) {
+  constexpr int L = R - U;
+  constexpr bool kWide = B128 && L >= 3;
+  constexpr int NP = kWide ? 1 : (L + 1) / 2;        // LDS blocks per (source, t)
+  constexpr int kBlkBytes = kWide ? 256 : 128;       // bytes of one block (16 entries)
+  constexpr int kTBytes = NP * kBlkBytes;            // bytes per (source, t)
+  constexpr int kSrcBytes = 8 * kTBytes;
+  constexpr int kEntry = kWide ? 16 : 8;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int K = a.K, KL = K - U;
+  // staging: dword index i of the LDS image
+  {
+    uint32_t* w = reinterpret_cast<uint32_t*>(lds);
+    const int n = KL * kSrcBytes / 4;
+    for (int i = threadIdx.x; i < n; i += kBlock) {
+      const int jj = i / (kSrcBytes / 4), rem = i % (kSrcBytes / 4);
+      const int t = rem / (kTBytes / 4), r2 = rem % (kTBytes / 4);
+      const int blk = r2 / (kBlkBytes / 4), r3 = r2 % (kBlkBytes / 4);
+      const int v = r3 / (kEntry / 4), word = r3 % (kEntry / 4);
+      const int lr = kWide ? word : 2 * blk + word;  // LDS row
+      const int row = lr + U, j = jj + U;
+      w[i] = lr < L ? a.wtab[size_t(row * K + j) * kNibWords + t * 16 + v] : 0u;
+    }
+  }
+  __syncthreads();
+  // the pointer table through the constant address space: scalar loads, even
+  // inside the column loop after stores (a generic load there is a vector
+  // load whose vmcnt(0) wait serialises every shard load issued before it)
+  const kptr* sp = (const kptr*)a.src;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[a.row0 + r];
+  const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(static_cast<void*>(lds)));
+  constexpr int kChunk = CHUNK;
+  const int64_t nblk = (a.nvec + kBlock - 1) / kBlock;
+  for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const int64_t col = b * kBlock + threadIdx.x;
+    if (col >= a.nvec) continue;
+    u32x4 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+    for (int j0 = 0; j0 < K; j0 += kChunk) {
+      u32x4 xs[kChunk];
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u)
+        if (j0 + u < K) xs[u] = load16t<1>(sp[j0 + u], col);
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u) {
+        const int j = j0 + u;
+        if (j >= K) break;
+        if (U == 1 && j == 0) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r] ^= xs[u];
+          continue;
+        }
+        if (U == 1) acc[0] ^= xs[u];
+        const uint32_t jbase = lds_base + uint32_t(j - U) * uint32_t(kSrcBytes);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t x = xs[u][c];
+          constexpr int kSh = kEntry == 16 ? 4 : 3;
+          constexpr uint32_t kNibMask = 0x0F0F0F0Fu << kSh;
+          const uint32_t ns[2] = {(x << kSh) & kNibMask, (x >> (4 - kSh)) & kNibMask};
+          // the eight lookups in HALVES groups, each folded before the next
+          // group's reads are issued (fewer live registers)
+#pragma unroll
+          for (int h = 0; h < HALVES; ++h) {
+            constexpr int TN = 8 / HALVES;
+            uint32_t v[TN][4];
+#pragma unroll
+            for (int tt = 0; tt < TN; ++tt) {
+              const int t = h * TN + tt;
+              const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
+                                  uint32_t(t * kTBytes);
+              if constexpr (kWide) {
+                const u32x4 q = *(lds_u32x4c*)(size_t(ad));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[tt][r] = q[r];
+              } else {
+#pragma unroll
+                for (int p = 0; p < NP; ++p) {
+                  if (2 * p + 1 < L) {
+                    const u32x2 q = *(lds_u32x2c*)(size_t(ad + p * kBlkBytes));
+                    v[tt][2 * p] = q.x;
+                    v[tt][2 * p + 1] = q.y;
+                  } else {
+                    v[tt][2 * p] = *(lds_u32c*)(size_t(ad + p * kBlkBytes));
+                  }
+                }
+              }
+            }
+#pragma unroll
+            for (int lr = 0; lr < L; ++lr) {
+              uint32_t e = acc[lr + U][c];
+#pragma unroll
+              for (int tt = 0; tt < TN; tt += 2) e = xor3(e, v[tt][lr], v[tt + 1][lr]);
+              acc[lr + U][c] = e;
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
+  }
+}
+
+template <int R, int U, bool B128>
+constexpr unsigned split_lds(int K) {
+  constexpr int L = R - U;
+  constexpr bool kWide = B128 && L >= 3;
+  constexpr int NP = kWide ? 1 : (L + 1) / 2;
+  return unsigned(K - U) * 8u * unsigned(NP * (kWide ? 256 : 128));
+}
+
+}  // namespace lab
+
+struct Variant {
+  std::string name;
+  const void* fn;
+  unsigned lds;
+};
+
+int main(int argc, char** argv) {
+  int w = 32, k = 10, m = 4, mib = 64, rounds = 7, reps = 10;
+  std::string only;
+  for (int i = 1; i + 1 < argc; i += 2) {
+    const std::string f = argv[i];
+    if (f == "--w") w = std::atoi(argv[i + 1]);
+    else if (f == "--k") k = std::atoi(argv[i + 1]);
+    else if (f == "--m") m = std::atoi(argv[i + 1]);
+    else if (f == "--mib") mib = std::atoi(argv[i + 1]);
+    else if (f == "--rounds") rounds = std::atoi(argv[i + 1]);
+    else if (f == "--reps") reps = std::atoi(argv[i + 1]);
+    else if (f == "--only") only = argv[i + 1];
+  }
+  if (m != 4 || k < 2 || k > 16 || (w != 32 && w != 16)) {
+    std::fprintf(stderr, "lab covers m = 4, 2 <= k <= 16, w = 16 / 32\n");
+    return 2;
+  }
+  const size_t S = size_t(mib) << 20, stride = S + (10 << 10);
+  const int R = m, K = k;
+  // Vandermonde coding matrix of the reference (reed_sol.cpp:63-84)
+  int* M = vandermonde_coding_matrix(k, m, w);
+  // per-coefficient nibble tables (ecgpu_runtime.hip build_wide_nib_tables)
+  std::vector<uint32_t> wtab(size_t(R) * K * kNibWords);
+  for (int r = 0; r < R; ++r)
+    for (int j = 0; j < K; ++j) {
+      const uint32_t c = uint32_t(M[r * k + j]);
+      uint32_t* t = &wtab[(size_t(r) * K + j) * kNibWords];
+      for (int tt = 0; tt < 8; ++tt)
+        for (uint32_t v = 0; v < 16; ++v)
+          t[tt * 16 + int(v)] = w == 32  ? gf_mul_poly(v << (4 * tt), c, 32)
+                                : tt < 4 ? gf_mul_poly(v << (4 * tt), c, 16)
+                                         : gf_mul_poly(v << (4 * (tt - 4)), c, 16) << 16;
+    }
+  bool unit_rc = true;
+  for (int j = 0; j < k; ++j) unit_rc = unit_rc && M[j] == 1;
+  for (int r = 0; r < m; ++r) unit_rc = unit_rc && M[r * k] == 1;
+
+  uint8_t* slab = nullptr;
+  CK(hipMalloc(&slab, stride * size_t(K + R) + 2 * stride));  // + a second output set for the checks
+  {
+    std::vector<uint8_t> h(S);
+    std::mt19937_64 g(1234);
+    for (int j = 0; j < K; ++j) {
+      for (size_t i = 0; i < S; i += 8) {
+        const uint64_t x = g();
+        std::memcpy(&h[i], &x, std::min<size_t>(8, S - i));
+      }
+      CK(hipMemcpy(slab + stride * j, h.data(), S, hipMemcpyHostToDevice));
+    }
+  }
+  std::vector<uint8_t*> hp(size_t(K + R));
+  for (int i = 0; i < K + R; ++i) hp[i] = slab + stride * size_t(i);
+  uint8_t** d_ptrs = nullptr;
+  CK(hipMalloc(&d_ptrs, sizeof(void*) * (K + R)));
+  CK(hipMemcpy(d_ptrs, hp.data(), sizeof(void*) * (K + R), hipMemcpyHostToDevice));
+  uint32_t* d_wtab = nullptr;
+  CK(hipMalloc(&d_wtab, wtab.size() * 4));
+  CK(hipMemcpy(d_wtab, wtab.data(), wtab.size() * 4, hipMemcpyHostToDevice));
+
+  ApplyArgs a{};
+  a.src = d_ptrs;
+  a.dst = d_ptrs + K;
+  a.nvec = int64_t(S / 16);
+  a.size = int64_t(S);
+  a.byte0 = a.nvec * 16;
+  a.src_stride = K;
+  a.dst_stride = R;
+  a.row0 = 0;
+  a.K = K;
+  a.R = R;
+  a.nt = 1;
+  a.wtab = d_wtab;
+
+  std::vector<Variant> vs;
+#define V(name, ...) \
+  vs.push_back({name, reinterpret_cast<const void*>(&lab::nib_split<__VA_ARGS__>), lab::split_lds<4, 0, true>(K)})
+#define VU(name, ...) \
+  vs.push_back({name, reinterpret_cast<const void*>(&lab::nib_split<__VA_ARGS__>), lab::split_lds<4, 1, true>(K)})
+  if (w == 32) {
+    vs.push_back({"prod_u0", reinterpret_cast<const void*>(&gf_apply_wide_nib<4>), unsigned(nib_lds_bytes(K, 4, 0))});
+    V("u0_c8", 4, 0, true, 8, 1, 1);
+    V("u0_c4_h4", 4, 0, true, 4, 4, 1);
+    V("u0_c4_h2", 4, 0, true, 4, 2, 1);
+    if (unit_rc) {
+      vs.push_back({"prod_u1", reinterpret_cast<const void*>(&gf_apply_wide_nib<4, 1>), unsigned(nib_lds_bytes(K, 4, 1))});
+      VU("u1_c10_h2", 4, 1, true, 10, 2, 1);
+      VU("u1_c4_h1", 4, 1, true, 4, 1, 1);
+      VU("u1_c4_h2", 4, 1, true, 4, 2, 1);
+      VU("u1_c4_h4", 4, 1, true, 4, 4, 1);
+      VU("u1_c5_h2_w6", 4, 1, true, 5, 2, 6);
+      VU("u1_c5_h4", 4, 1, true, 5, 4, 1);
+      VU("u1_c3_h2", 4, 1, true, 3, 2, 1);
+      VU("u1_c2_h4", 4, 1, true, 2, 4, 1);
+    }
+  } else {
+    vs.push_back({"prod_nib16_4", reinterpret_cast<const void*>(&gf_apply_wide_nib16<4>), unsigned(K * nib16_source_bytes(4))});
+  }
+  int dev = 0, cus = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  auto grid_of = [&](const Variant& v) {
+    int n = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, v.fn, kBlock, v.lds));
+    return std::max(1, n) * cus;
+  };
+  auto launch = [&](const Variant& v, ApplyArgs args) {
+    void* kargs[] = {&args};
+    CK(hipLaunchKernel(v.fn, dim3(unsigned(grid_of(v)), 1), dim3(kBlock), kargs, v.lds, nullptr));
+  };
+  // reference outputs from the production kernel, then a host spot check
+  launch(vs[0], a);
+  CK(hipDeviceSynchronize());
+  std::vector<std::vector<uint8_t>> want(static_cast<size_t>(R), std::vector<uint8_t>(S));
+  for (int r = 0; r < R; ++r) CK(hipMemcpy(want[r].data(), hp[size_t(K + r)], S, hipMemcpyDeviceToHost));
+  {
+    std::vector<uint32_t> col(static_cast<size_t>(K));
+    std::mt19937_64 g(99);
+    for (int n = 0; n < 2000; ++n) {
+      const size_t off = (g() % (S / 4)) * 4;
+      for (int j = 0; j < K; ++j) CK(hipMemcpy(&col[j], hp[j] + off, 4, hipMemcpyDeviceToHost));
+      for (int r = 0; r < R; ++r) {
+        uint32_t e = 0;
+        for (int j = 0; j < K; ++j) {
+          if (w == 32) {
+            e ^= gf_mul_poly(col[j], uint32_t(M[r * k + j]), 32);
+          } else {
+            e ^= gf_mul_poly(col[j] & 0xFFFF, uint32_t(M[r * k + j]), 16) |
+                 (gf_mul_poly(col[j] >> 16, uint32_t(M[r * k + j]), 16) << 16);
+          }
+        }
+        uint32_t got;
+        std::memcpy(&got, &want[r][off], 4);
+        if (got != e) {
+          std::fprintf(stderr, "production kernel disagrees with the host at row %d offset %zu\n", r, off);
+          return 1;
+        }
+      }
+    }
+  }
+  for (size_t i = 1; i < vs.size(); ++i) {
+    CK(hipMemset(slab + stride * size_t(K), 0, stride * size_t(R)));
+    launch(vs[i], a);
+    CK(hipDeviceSynchronize());
+    std::vector<uint8_t> got(S);
+    for (int r = 0; r < R; ++r) {
+      CK(hipMemcpy(got.data(), hp[size_t(K + r)], S, hipMemcpyDeviceToHost));
+      if (got != want[r]) {
+        std::fprintf(stderr, "variant %s differs at row %d\n", vs[i].name.c_str(), r);
+        return 1;
+      }
+    }
+  }
+  // timing: interleaved rounds, reps launches each, median per launch
+  std::vector<std::vector<float>> t(vs.size());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int rd = 0; rd < rounds; ++rd)
+    for (size_t i = 0; i < vs.size(); ++i) {
+      if (!only.empty() && vs[i].name.find(only) == std::string::npos && i != 0) continue;
+      for (int q = 0; q < 2; ++q) launch(vs[i], a);  // warm
+      for (int q = 0; q < reps; ++q) {
+        CK(hipEventRecord(e0, nullptr));
+        launch(vs[i], a);
+        CK(hipEventRecord(e1, nullptr));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t[i].push_back(ms * 1000.f);
+      }
+    }
+  const double bytes = double(K + R) * double(S);
+  for (size_t i = 0; i < vs.size(); ++i) {
+    if (t[i].empty()) continue;
+    std::sort(t[i].begin(), t[i].end());
+    const double med = t[i][t[i].size() / 2], mn = t[i][0];
+    int n = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, vs[i].fn, kBlock, vs[i].lds));
+    std::printf("{\"w\": %d, \"k\": %d, \"m\": %d, \"shard_mib\": %d, \"variant\": \"%s\", \"lds\": %u, "
+                "\"blocks_per_cu\": %d, \"median_us\": %.1f, \"min_us\": %.1f, \"GBps\": %.0f, \"samples\": %zu}\n",
+                w, k, m, mib, vs[i].name.c_str(), vs[i].lds, n, med, mn, bytes / med / 1e3, t[i].size());
+  }
+  return 0;
+}

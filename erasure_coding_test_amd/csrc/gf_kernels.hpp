@@ -1089,16 +1089,16 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets16(PacketArgs a) {
   for (; j + CHUNK <= a.nsrc; j += CHUNK) {
     u32x4 x[CHUNK];
 #pragma unroll
-    for (int u = 0; u < CHUNK; ++u) x[u] = load16t<1>(kload(a.src, j + u) + soff, 0);
+    for (int u = 0; u < CHUNK; ++u) x[u] = load16t<1>(a.src[j + u] + soff, 0);
 #pragma unroll
-    for (int u = 0; u < CHUNK; ++u) xor_masked16<RT, CHUNK>(acc, x[u], kload(a.mask, j + u));
+    for (int u = 0; u < CHUNK; ++u) xor_masked16<RT, CHUNK>(acc, x[u], a.mask[j + u]);
   }
-  for (; j < a.nsrc; ++j) xor_masked16<RT, CHUNK>(acc, load16t<1>(kload(a.src, j) + soff, 0), kload(a.mask, j));
+  for (; j < a.nsrc; ++j) xor_masked16<RT, CHUNK>(acc, load16t<1>(a.src[j] + soff, 0), a.mask[j]);
   // output pointers only now: held across the loop they would take RT SGPR
-  // pairs from the row selectors (kload: scalar loads between the stores)
+  // pairs from the row selectors (no store precedes these scalar loads)
 #pragma unroll
   for (int r = 0; r < RT; ++r)
-    if (r < a.R) store16t<1>(kload(a.dst, r) + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+    if (r < a.R) store16t<1>(a.dst[r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
 }
 
 // Production 16-B form (packets, strides and bases 16-B aligned): source
@@ -1125,8 +1125,8 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets16p(PacketArgs a) {
     const int b = (c < nc ? c : nc - 1) * 4;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      m[u] = kload(a.mask, b + u);
-      x[u] = load16t<1>(kload(a.src, b + u) + soff, 0);
+      m[u] = a.mask[b + u];
+      x[u] = load16t<1>(a.src[b + u] + soff, 0);
     }
   };
   auto apply4 = [&](const u32x4 (&x)[4], const uint32_t (&m)[4]) {
@@ -1143,10 +1143,10 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets16p(PacketArgs a) {
       apply4(xb, mb);
     }
   }
-  for (int j = nc * 4; j < a.nsrc; ++j) xor_masked16<RT, 4>(acc, load16t<1>(kload(a.src, j) + soff, 0), kload(a.mask, j));
+  for (int j = nc * 4; j < a.nsrc; ++j) xor_masked16<RT, 4>(acc, load16t<1>(a.src[j] + soff, 0), a.mask[j]);
 #pragma unroll
   for (int r = 0; r < RT; ++r)
-    if (r < a.R) store16t<1>(kload(a.dst, r) + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+    if (r < a.R) store16t<1>(a.dst[r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
 }
 
 // Byte form for packet sizes / bases that are not 8-byte aligned.

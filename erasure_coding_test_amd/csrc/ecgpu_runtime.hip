@@ -489,8 +489,20 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
           // exactly one resident round of workgroups (occupancy x CUs), each
           // looping over column blocks: a second, partial round would run
           // on part of the chip
-          const int64_t per_stripe =
-              std::max<int64_t>(1, int64_t(multiprocessors(p->device)) * resident_blocks(vec_fn, nib_lds) / ns);
+          // The w = 16 packed kernel (LDS at half the w = 32 cycles, HBM-bound)
+          // runs fewer workgroups per CU than fit, like the w = 8 residency
+          // cap: 3 per CU beat the 6 the occupancy allows for RS(10,4) 64 MiB
+          // (171.5 vs 181.6 us), RS(5,4) 64 MiB (107.3 vs 116.0) and RS(12,4)
+          // 16 MiB (55.1 vs 56.3; tools/wide_lab.hip grid sweep,
+          // profiles/r03_wide_lab.jsonl); the LDS-bound w = 32 kernel wants
+          // every wave it can get (3 per CU: 242 vs 192 us).
+          // ECGPU_WIDE16_BPCU overrides (0: the occupancy).
+          int bpcu = resident_blocks(vec_fn, nib_lds);
+          if (pack16) {
+            const int cap16 = env_int("ECGPU_WIDE16_BPCU", 3);
+            if (cap16 > 0) bpcu = std::min(bpcu, cap16);
+          }
+          const int64_t per_stripe = std::max<int64_t>(1, int64_t(multiprocessors(p->device)) * bpcu / ns);
           const dim3 grid(unsigned(std::min(nblk, per_stripe)), unsigned(ns));
           ECGPU_HIP(launch(vec_fn, grid, block, a, stream, nib_lds));
         } else {

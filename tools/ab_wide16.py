@@ -1,0 +1,69 @@
+"""In-process A/B of the w = 16 packed nibble kernel's grid cap
+(ECGPU_WIDE16_BPCU, read per launch) on two shard layouts: separately
+allocated 64 MiB tensors (what a caller passing malloc'd shards gets) and the
+library's skewed stripe slab.  Run under rocprofv3 --kernel-trace; launches
+are attributed by order (rounds x layouts x settings x reps).
+
+    rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ab16 -o run -- python3 tools/ab_wide16.py
+    python3 tools/ab_wide16.py --summarize gpurun_out/ab16
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SETTINGS = ["0", "3", "4"]
+LAYOUTS = ["separate", "slab"]
+ROUNDS, REPS = 6, 5
+
+
+def run():
+    import torch
+
+    import erasure_coding_test_amd as E
+    k, m, w, S = 10, 4, 16, 64 << 20
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w)
+    sep_d = [torch.randint(0, 256, (S,), dtype=torch.uint8, device="cuda") for _ in range(k)]
+    sep_c = [torch.empty(S, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    slab, shards = E.alloc_stripes(1, k, m, S)
+    slab.random_(0, 256)
+    lay = {"separate": (sep_d, sep_c), "slab": (shards[0][:k], shards[0][k:])}
+    for _ in range(ROUNDS):
+        for L in LAYOUTS:
+            d, c = lay[L]
+            for st in SETTINGS:
+                os.environ["ECGPU_WIDE16_BPCU"] = st
+                for _ in range(REPS):
+                    E.jerasure.jerasure_matrix_encode(k, m, w, M, d, c, S)
+    torch.cuda.synchronize()
+
+
+def summarize(d):
+    f = glob.glob(os.path.join(d, "**", "run_kernel_trace.csv"), recursive=True)[0]
+    rows = [r for r in csv.DictReader(open(f)) if "gf_apply_wide_nib16" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+    out, i = {}, 0
+    for _ in range(ROUNDS):
+        for L in LAYOUTS:
+            for st in SETTINGS:
+                out.setdefault(f"{L} bpcu={st}", []).extend(durs[i:i + REPS])
+                i += REPS
+    res = {key: {"median_us": round(statistics.median(v), 1), "min_us": round(min(v), 1), "n": len(v)}
+           for key, v in out.items()}
+    print(json.dumps({"kernel": "gf_apply_wide_nib16<4>, RS(10,4) w=16 64 MiB encode", "launches": len(durs),
+                      "results": res}, indent=1))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--summarize")
+    a = ap.parse_args()
+    summarize(a.summarize) if a.summarize else run()

@@ -158,6 +158,97 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   }
 }
 
+
+// w = 16 packed-pair kernel (gf_apply_wide_nib16) with the source chunk and
+// the lookup grouping as parameters.
+template <int R, int CHUNK, int GROUPS, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void nib16v(ApplyArgs a) {
+  constexpr int EW = nib16_entry_words(R), EB = 4 * EW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int K = a.K;
+  const int n = K * kNibWords * EW;
+  for (int i = threadIdx.x; i < n; i += kBlock) {
+    const int pr = i % EW, e = (i / EW) % kNibWords, j = i / (EW * kNibWords);
+    const bool high = (e >> 4) >= 4;
+    auto word = [&](int r) -> uint32_t {
+      if (r >= R) return 0u;
+      const uint32_t v = a.wtab[size_t(r * K + j) * kNibWords + e];
+      return high ? (v >> 16) : (v & 0xFFFFu);
+    };
+    reinterpret_cast<uint32_t*>(lds)[i] = word(2 * pr) | (word(2 * pr + 1) << 16);
+  }
+  __syncthreads();
+  const kptr* sp = (const kptr*)a.src;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[a.row0 + r];
+  const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(static_cast<void*>(lds)));
+  const int64_t nblk = (a.nvec + kBlock - 1) / kBlock;
+  for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const int64_t col = b * kBlock + threadIdx.x;
+    if (col >= a.nvec) continue;
+    uint32_t lo[4][EW], hi[4][EW];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int q = 0; q < EW; ++q) lo[c][q] = hi[c][q] = 0u;
+    for (int j0 = 0; j0 < K; j0 += CHUNK) {
+      u32x4 xs[CHUNK];
+#pragma unroll
+      for (int u = 0; u < CHUNK; ++u)
+        if (j0 + u < K) xs[u] = load16t<1>(sp[j0 + u], col);
+#pragma unroll
+      for (int u = 0; u < CHUNK; ++u) {
+        const int j = j0 + u;
+        if (j >= K) break;
+        const uint32_t jbase = lds_base + uint32_t(j) * uint32_t(nib16_source_bytes(R));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t x = xs[u][c];
+          constexpr int kSh = EB == 8 ? 3 : 2;
+          constexpr uint32_t kNibMask = 0x0F0F0F0Fu << kSh;
+          const uint32_t ns[2] = {(x << kSh) & kNibMask, (x >> (4 - kSh)) & kNibMask};
+#pragma unroll
+          for (int g = 0; g < GROUPS; ++g) {
+            constexpr int TN = 8 / GROUPS;
+            uint32_t v[TN][EW];
+#pragma unroll
+            for (int tt = 0; tt < TN; ++tt) {
+              const int t = g * TN + tt;
+              const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
+                                  uint32_t(t * 16 * EB);
+              if constexpr (EW == 1) {
+                v[tt][0] = *(lds_u32c*)(size_t(ad));
+              } else {
+                const u32x2 q = *(lds_u32x2c*)(size_t(ad));
+                v[tt][0] = q.x;
+                v[tt][1] = q.y;
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < EW; ++q) {
+#pragma unroll
+              for (int tt = 0; tt < TN; tt += 2) {
+                const int t = g * TN + tt;
+                if (t < 4) lo[c][q] = xor3(lo[c][q], v[tt][q], v[tt + 1][q]);
+                else hi[c][q] = xor3(hi[c][q], v[tt][q], v[tt + 1][q]);
+              }
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      u32x4 o;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        o[c] = __builtin_amdgcn_perm(hi[c][r >> 1], lo[c][r >> 1], (r & 1) ? 0x07060302u : 0x05040100u);
+      store16t<1>(dp[r], col, o);
+    }
+  }
+}
+
 template <int R, int U, bool B128>
 constexpr unsigned split_lds(int K) {
   constexpr int L = R - U;
@@ -172,6 +263,7 @@ struct Variant {
   std::string name;
   const void* fn;
   unsigned lds;
+  int bpcu = 0;  // > 0: grid of bpcu workgroups per CU (fewer resident than the occupancy allows)
 };
 
 int main(int argc, char** argv) {
@@ -259,6 +351,9 @@ int main(int argc, char** argv) {
     V("u0_c4_h2", 4, 0, true, 4, 2, 1);
     if (unit_rc) {
       vs.push_back({"prod_u1", reinterpret_cast<const void*>(&gf_apply_wide_nib<4, 1>), unsigned(nib_lds_bytes(K, 4, 1))});
+      for (int b : {2, 3, 4, 5})
+        vs.push_back({"prod_u1_grid" + std::to_string(b), reinterpret_cast<const void*>(&gf_apply_wide_nib<4, 1>),
+                      unsigned(nib_lds_bytes(K, 4, 1)), b});
       VU("u1_c10_h2", 4, 1, true, 10, 2, 1);
       VU("u1_c4_h1", 4, 1, true, 4, 1, 1);
       VU("u1_c4_h2", 4, 1, true, 4, 2, 1);
@@ -269,7 +364,19 @@ int main(int argc, char** argv) {
       VU("u1_c2_h4", 4, 1, true, 2, 4, 1);
     }
   } else {
-    vs.push_back({"prod_nib16_4", reinterpret_cast<const void*>(&gf_apply_wide_nib16<4>), unsigned(K * nib16_source_bytes(4))});
+    const unsigned l16 = unsigned(K * nib16_source_bytes(4));
+    vs.push_back({"prod_nib16_4", reinterpret_cast<const void*>(&gf_apply_wide_nib16<4>), l16});
+    vs.push_back({"n16_c8_g1", reinterpret_cast<const void*>(&lab::nib16v<4, 8, 1>), l16});
+    vs.push_back({"n16_c4_g1", reinterpret_cast<const void*>(&lab::nib16v<4, 4, 1>), l16});
+    vs.push_back({"n16_c4_g2", reinterpret_cast<const void*>(&lab::nib16v<4, 4, 2>), l16});
+    vs.push_back({"n16_c2_g2", reinterpret_cast<const void*>(&lab::nib16v<4, 2, 2>), l16});
+    vs.push_back({"n16_c5_g2", reinterpret_cast<const void*>(&lab::nib16v<4, 5, 2>), l16});
+    vs.push_back({"n16_c10_g2", reinterpret_cast<const void*>(&lab::nib16v<4, 10, 2>), l16});
+    vs.push_back({"n16_c4_g2_w8", reinterpret_cast<const void*>(&lab::nib16v<4, 4, 2, 8>), l16});
+    for (int b : {2, 3, 4, 5})
+      vs.push_back({"prod_nib16_4_grid" + std::to_string(b), reinterpret_cast<const void*>(&gf_apply_wide_nib16<4>), l16, b});
+    for (int b : {2, 3, 4})
+      vs.push_back({"n16_c2_g2_grid" + std::to_string(b), reinterpret_cast<const void*>(&lab::nib16v<4, 2, 2>), l16, b});
   }
   int dev = 0, cus = 0;
   CK(hipGetDevice(&dev));
@@ -277,6 +384,7 @@ int main(int argc, char** argv) {
   auto grid_of = [&](const Variant& v) {
     int n = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, v.fn, kBlock, v.lds));
+    if (v.bpcu > 0) n = std::min(n, v.bpcu);
     return std::max(1, n) * cus;
   };
   auto launch = [&](const Variant& v, ApplyArgs args) {
@@ -352,6 +460,7 @@ int main(int argc, char** argv) {
     const double med = t[i][t[i].size() / 2], mn = t[i][0];
     int n = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, vs[i].fn, kBlock, vs[i].lds));
+    if (vs[i].bpcu > 0) n = std::min(n, vs[i].bpcu);
     std::printf("{\"w\": %d, \"k\": %d, \"m\": %d, \"shard_mib\": %d, \"variant\": \"%s\", \"lds\": %u, "
                 "\"blocks_per_cu\": %d, \"median_us\": %.1f, \"min_us\": %.1f, \"GBps\": %.0f, \"samples\": %zu}\n",
                 w, k, m, mib, vs[i].name.c_str(), vs[i].lds, n, med, mn, bytes / med / 1e3, t[i].size());

@@ -84,6 +84,7 @@ __global__ __launch_bounds__(kBlock) void packets16p_r2(PacketArgs a) {
 struct Variant {
   std::string name;
   const void* fn;
+  unsigned lds = 0;  // dynamic LDS per workgroup: an unused allocation that caps residency
 };
 
 int main(int argc, char** argv) {
@@ -145,12 +146,17 @@ int main(int argc, char** argv) {
   a.R = R;
 
   std::vector<Variant> vs = {{"prod_packets16p", reinterpret_cast<const void*>(&gf_xor_packets16p<32>)},
-                             {"r2_packets16p", reinterpret_cast<const void*>(&lab::packets16p_r2<32>)},
                              {"prod_packets16_c8", reinterpret_cast<const void*>(&gf_xor_packets16<32, 8>)}};
+  int dev = 0, lds_cu = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+  for (int b : {1, 2})
+    vs.push_back({"prod_packets16p_cap" + std::to_string(b), reinterpret_cast<const void*>(&gf_xor_packets16p<32>),
+                  unsigned(lds_cu / b) & ~511u});
   auto launch = [&](const Variant& v) {
     PacketArgs args = a;
     void* kargs[] = {&args};
-    CK(hipLaunchKernel(v.fn, dim3(unsigned((a.ncols + kBlock - 1) / kBlock)), dim3(kBlock), kargs, 0, nullptr));
+    CK(hipLaunchKernel(v.fn, dim3(unsigned((a.ncols + kBlock - 1) / kBlock)), dim3(kBlock), kargs, v.lds, nullptr));
   };
   launch(vs[0]);
   CK(hipDeviceSynchronize());

@@ -1,0 +1,231 @@
+// encode_lab.hip -- A/B lab for the production w = 8 encode kernel's launch
+// shape on the bench's C3 layout (96 stripes x RS(10,4) x 4 MiB shards at the
+// library's skewed stride): workgroup size (256 / 512 / 1024 threads, i.e. 4 /
+// 8 / 16 KiB contiguous per shard per workgroup) and resident workgroups per
+// CU (an unused dynamic LDS allocation).  Every variant is checked bit-exact
+// against the production launch, then timed in interleaved rounds with HIP
+// events.
+//
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I erasure_coding_test_amd/csrc \
+//     tools/encode_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp erasure_coding_test_amd/csrc/matrix_host.cpp \
+//     -o tools/encode_lab.bin
+//   tools/encode_lab.bin [--stripes 96] [--rounds 7] [--reps 10]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "gf_host.hpp"
+#include "gf_kernels.hpp"
+#include "matrix_host.hpp"
+
+using namespace ecgpu;
+using namespace ecgpu::dev;
+
+#define CK(x)                                                                                 \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) {                                                                   \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(1);                                                                           \
+    }                                                                                         \
+  } while (0)
+
+namespace lab {
+// gf_apply<K, R, UNITS> (VEC 1, 3-bit slices, nt loads and stores) with a
+// BS-thread workgroup.
+template <int K, int R, int UNITS, int BS>
+__global__ __launch_bounds__(BS) void enc_bs(ApplyArgs a) {
+  const int64_t col = int64_t(blockIdx.x) * BS + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = load16t<1>(sp[j], col);
+  combine_store<K, R, UNITS, 3, 1>(a, x, dp, col);
+}
+}  // namespace lab
+
+struct Variant {
+  std::string name;
+  const void* fn;
+  int bs;
+  int blocks_per_cu;  // 0: uncapped
+};
+
+// builds the production 3-bit-slice tables (ecgpu_runtime.hip build_tables)
+static void build_p3(int c, uint32_t* p3) {
+  const auto& T = gf8().mul[c & 0xFF];
+  for (int i = 0; i < kP3Words; ++i) p3[i] = 0;
+  for (int e = 0; e < 8; ++e) {
+    p3[e >> 2] |= uint32_t(T[e]) << (8 * (e & 3));
+    p3[2 + (e >> 2)] |= uint32_t(T[e << 3]) << (8 * (e & 3));
+  }
+  for (int e = 0; e < 4; ++e) p3[4] |= uint32_t(T[e << 6]) << (8 * e);
+}
+
+int main(int argc, char** argv) {
+  int stripes = 96, rounds = 7, reps = 10;
+  for (int i = 1; i + 1 < argc; i += 2) {
+    const std::string f = argv[i];
+    if (f == "--stripes") stripes = std::atoi(argv[i + 1]);
+    else if (f == "--rounds") rounds = std::atoi(argv[i + 1]);
+    else if (f == "--reps") reps = std::atoi(argv[i + 1]);
+  }
+  constexpr int k = 10, m = 4;
+  const size_t S = size_t(4) << 20, stride = S + (10 << 10);
+  int* M = vandermonde_coding_matrix(k, m, 8);
+  std::vector<uint32_t> ptab(size_t(m) * k * kP3Words);
+  for (int r = 0; r < m; ++r)
+    for (int j = 0; j < k; ++j) build_p3(M[r * k + j], &ptab[(size_t(r) * k + j) * kP3Words]);
+  uint8_t* slab = nullptr;
+  const size_t slab_bytes = stride * size_t(k + m) * size_t(stripes);
+  CK(hipMalloc(&slab, slab_bytes));
+  {
+    std::vector<uint8_t> h(S);
+    std::mt19937_64 g(11);
+    for (size_t i = 0; i < S; i += 8) {
+      const uint64_t x = g();
+      std::memcpy(&h[i], &x, 8);
+    }
+    for (int s = 0; s < stripes; ++s)
+      for (int j = 0; j < k; ++j) {
+        h[size_t(s * k + j) % S] ^= 0x5A;  // stripes differ
+        CK(hipMemcpy(slab + stride * (size_t(s) * (k + m) + j), h.data(), S, hipMemcpyHostToDevice));
+      }
+  }
+  std::vector<const uint8_t*> hs;
+  std::vector<uint8_t*> hd;
+  for (int s = 0; s < stripes; ++s) {
+    for (int j = 0; j < k; ++j) hs.push_back(slab + stride * (size_t(s) * (k + m) + j));
+    for (int r = 0; r < m; ++r) hd.push_back(slab + stride * (size_t(s) * (k + m) + k + r));
+  }
+  const uint8_t** d_src = nullptr;
+  uint8_t** d_dst = nullptr;
+  uint32_t* d_ptab = nullptr;
+  CK(hipMalloc(&d_src, sizeof(void*) * hs.size()));
+  CK(hipMalloc(&d_dst, sizeof(void*) * hd.size()));
+  CK(hipMalloc(&d_ptab, 4 * ptab.size()));
+  CK(hipMemcpy(d_src, hs.data(), sizeof(void*) * hs.size(), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_dst, hd.data(), sizeof(void*) * hd.size(), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_ptab, ptab.data(), 4 * ptab.size(), hipMemcpyHostToDevice));
+  ApplyArgs a{};
+  a.ptab = d_ptab;
+  a.src = d_src;
+  a.dst = d_dst;
+  a.nvec = int64_t(S / 16);
+  a.size = int64_t(S);
+  a.byte0 = a.nvec * 16;
+  a.src_stride = k;
+  a.dst_stride = m;
+  a.row0 = 0;
+  a.K = k;
+  a.R = m;
+  a.nt = 1;
+  constexpr int U = kUnitCol0 | kUnitRow0;
+  std::vector<Variant> vs = {
+      {"prod_bs256_cap3", reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>), 256, 3},
+      {"bs256_cap4", reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>), 256, 4},
+      {"bs256_cap2", reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>), 256, 2},
+      {"bs512_cap1", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 512>), 512, 1},
+      {"bs512_cap2", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 512>), 512, 2},
+      {"bs512_cap3", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 512>), 512, 3},
+      {"bs1024_cap1", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 1024>), 1024, 1},
+      {"bs1024_cap2", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 1024>), 1024, 2},
+  };
+  int dev = 0, lds_cu = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+  auto lds_of = [&](const Variant& v) -> unsigned {
+    if (v.blocks_per_cu <= 0) return 0u;
+    const unsigned b = unsigned(lds_cu / v.blocks_per_cu) & ~511u;
+    return b > unsigned(lds_cu / (v.blocks_per_cu + 1)) ? b : 0u;
+  };
+  auto launch = [&](const Variant& v) {
+    ApplyArgs args = a;
+    void* kargs[] = {&args};
+    const dim3 grid(unsigned((a.nvec + v.bs - 1) / v.bs), unsigned(stripes));
+    CK(hipLaunchKernel(v.fn, grid, dim3(unsigned(v.bs)), kargs, lds_of(v), nullptr));
+  };
+  // reference: the production launch; spot-check it against the host
+  launch(vs[0]);
+  CK(hipDeviceSynchronize());
+  std::vector<uint8_t> want(S), got(S);
+  {
+    std::mt19937_64 g(5);
+    for (int n = 0; n < 200; ++n) {
+      const int s = int(g() % size_t(stripes));
+      const size_t b = g() % S;
+      uint8_t col[k];
+      for (int j = 0; j < k; ++j) CK(hipMemcpy(&col[j], hs[size_t(s * k + j)] + b, 1, hipMemcpyDeviceToHost));
+      for (int r = 0; r < m; ++r) {
+        uint8_t e = 0;
+        for (int j = 0; j < k; ++j) e ^= uint8_t(single_multiply(M[r * k + j], col[j], 8));
+        uint8_t o;
+        CK(hipMemcpy(&o, hd[size_t(s * m + r)] + b, 1, hipMemcpyDeviceToHost));
+        if (o != e) {
+          std::fprintf(stderr, "production launch disagrees with the host\n");
+          return 1;
+        }
+      }
+    }
+  }
+  // every variant must reproduce the production outputs (two stripes compared whole)
+  std::vector<std::vector<uint8_t>> ref;
+  for (int s : {0, stripes - 1})
+    for (int r = 0; r < m; ++r) {
+      ref.emplace_back(S);
+      CK(hipMemcpy(ref.back().data(), hd[size_t(s * m + r)], S, hipMemcpyDeviceToHost));
+    }
+  for (size_t v = 1; v < vs.size(); ++v) {
+    for (int s : {0, stripes - 1})
+      for (int r = 0; r < m; ++r) CK(hipMemset(hd[size_t(s * m + r)], 0, S));
+    launch(vs[v]);
+    CK(hipDeviceSynchronize());
+    size_t i = 0;
+    for (int s : {0, stripes - 1})
+      for (int r = 0; r < m; ++r) {
+        CK(hipMemcpy(got.data(), hd[size_t(s * m + r)], S, hipMemcpyDeviceToHost));
+        if (got != ref[i++]) {
+          std::fprintf(stderr, "variant %s differs\n", vs[v].name.c_str());
+          return 1;
+        }
+      }
+  }
+  std::vector<std::vector<float>> t(vs.size());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int rd = 0; rd < rounds; ++rd)
+    for (size_t v = 0; v < vs.size(); ++v) {
+      for (int q = 0; q < 2; ++q) launch(vs[v]);
+      for (int q = 0; q < reps; ++q) {
+        CK(hipEventRecord(e0, nullptr));
+        launch(vs[v]);
+        CK(hipEventRecord(e1, nullptr));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t[v].push_back(ms * 1000.f);
+      }
+    }
+  const double bytes = double(k + m) * double(S) * stripes;
+  for (size_t v = 0; v < vs.size(); ++v) {
+    std::sort(t[v].begin(), t[v].end());
+    const double med = t[v][t[v].size() / 2];
+    std::printf("{\"variant\": \"%s\", \"block\": %d, \"blocks_per_cu\": %d, \"stripes\": %d, \"median_us\": %.1f, "
+                "\"min_us\": %.1f, \"GBps\": %.0f, \"frac\": %.4f}\n",
+                vs[v].name.c_str(), vs[v].bs, vs[v].blocks_per_cu, stripes, med, double(t[v][0]),
+                bytes / med / 1e3, bytes / med / 1e3 / 8000.0);
+  }
+  return 0;
+}

@@ -152,7 +152,20 @@ def dist_setup():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo prints its connection report ("[Gloo] Rank r is connected to
+        # ...") on stdout, where the launcher reads this bench's one JSON
+        # line; the ranks' reports interleave.  Send it to stderr: fd 1 points
+        # at fd 2 until every rank has connected (the barrier).
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     return rank, local, world
 
 

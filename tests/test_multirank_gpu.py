@@ -141,8 +141,9 @@ def _bench(args, env_extra=None, timeout=180):
 
 
 def _line(out):
-    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, out
+    # stdout is exactly the one JSON line (gloo's connection reports go to stderr)
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out
     return json.loads(lines[0])
 
 

@@ -10,6 +10,8 @@
 //     tools/encode_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp erasure_coding_test_amd/csrc/matrix_host.cpp \
 //     -o tools/encode_lab.bin
 //   tools/encode_lab.bin [--stripes 96] [--rounds 7] [--reps 10]
+//   tools/encode_lab.bin --skews 10,12,8,6 [--k 12 --m 4 --mib 16 --stripes 24]
+//       the production launch on one slab per shard-stride skew (KiB), interleaved
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -73,13 +75,39 @@ static void build_p3(int c, uint32_t* p3) {
   for (int e = 0; e < 4; ++e) p3[4] |= uint32_t(T[e << 6]) << (8 * e);
 }
 
+template <int k, int m>
+int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int reps);
+
 int main(int argc, char** argv) {
-  int stripes = 96, rounds = 7, reps = 10;
+  int stripes = 96, rounds = 7, reps = 10, kk = 10, mm = 4, kib = 4096;
+  std::vector<int> skews;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string f = argv[i];
     if (f == "--stripes") stripes = std::atoi(argv[i + 1]);
     else if (f == "--rounds") rounds = std::atoi(argv[i + 1]);
     else if (f == "--reps") reps = std::atoi(argv[i + 1]);
+    else if (f == "--k") kk = std::atoi(argv[i + 1]);
+    else if (f == "--m") mm = std::atoi(argv[i + 1]);
+    else if (f == "--mib") kib = 1024 * std::atoi(argv[i + 1]);
+    else if (f == "--kib") kib = std::atoi(argv[i + 1]);
+    else if (f == "--skews") {
+      std::string v = argv[i + 1];
+      size_t p = 0;
+      while (p < v.size()) {
+        const size_t q = v.find(',', p);
+        skews.push_back(std::atoi(v.substr(p, q - p).c_str()));
+        p = q == std::string::npos ? v.size() : q + 1;
+      }
+    }
+  }
+  if (!skews.empty()) {
+    if (stripes <= 0) stripes = std::max(1, int((5ll << 30) / ((long long)(kk + mm) * kib * 1024)));  // ~5 GiB per launch
+    if (kk == 10 && mm == 4) return skew_ab<10, 4>(stripes, kib, skews, rounds, reps);
+    if (kk == 12 && mm == 4) return skew_ab<12, 4>(stripes, kib, skews, rounds, reps);
+    if (kk == 6 && mm == 3) return skew_ab<6, 3>(stripes, kib, skews, rounds, reps);
+    if (kk == 4 && mm == 2) return skew_ab<4, 2>(stripes, kib, skews, rounds, reps);
+    std::fprintf(stderr, "skew A/B covers RS(10,4), RS(12,4), RS(6,3), RS(4,2)\n");
+    return 2;
   }
   constexpr int k = 10, m = 4;
   const size_t S = size_t(4) << 20, stride = S + (10 << 10);
@@ -226,6 +254,129 @@ int main(int argc, char** argv) {
                 "\"min_us\": %.1f, \"GBps\": %.0f, \"frac\": %.4f}\n",
                 vs[v].name.c_str(), vs[v].bs, vs[v].blocks_per_cu, stripes, med, double(t[v][0]),
                 bytes / med / 1e3, bytes / med / 1e3 / 8000.0);
+  }
+  return 0;
+}
+
+// One slab per skew, the production launch (unit structure col 0 / row 0,
+// nt loads and stores, the library's residency rule) on each, interleaved.
+// Parity of every slab's first and last stripe is checked against the host.
+template <int k, int m>
+int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int reps) {
+  const size_t S = size_t(kib) << 10;
+  int* M = vandermonde_coding_matrix(k, m, 8);
+  std::vector<uint32_t> ptab(size_t(m) * k * kP3Words);
+  for (int r = 0; r < m; ++r)
+    for (int j = 0; j < k; ++j) build_p3(M[r * k + j], &ptab[(size_t(r) * k + j) * kP3Words]);
+  uint32_t* d_ptab = nullptr;
+  CK(hipMalloc(&d_ptab, 4 * ptab.size()));
+  CK(hipMemcpy(d_ptab, ptab.data(), 4 * ptab.size(), hipMemcpyHostToDevice));
+  int dev = 0, lds_cu = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+  const int blocks = k + m <= 9 ? 4 : 3;  // ecgpu_runtime.hip residency_lds_bytes
+  const unsigned lds = unsigned(lds_cu / blocks) & ~511u;
+  constexpr int U = kUnitCol0 | kUnitRow0;
+  const void* fn = reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>);
+  struct Slab {
+    int skew;
+    uint8_t* base;
+    size_t stride;
+    ApplyArgs a;
+    std::vector<float> t;
+  };
+  std::vector<Slab> slabs;
+  std::vector<uint8_t> h(S);
+  std::mt19937_64 g(17);
+  for (size_t i = 0; i < S; i += 8) {
+    const uint64_t x = g();
+    std::memcpy(&h[i], &x, 8);
+  }
+  for (int sk : skews) {
+    Slab sl{};
+    sl.skew = sk;
+    sl.stride = ((S + 255) & ~size_t(255)) + size_t(sk) * 1024;
+    CK(hipMalloc(&sl.base, sl.stride * size_t(k + m) * size_t(stripes)));
+    std::vector<const uint8_t*> hs;
+    std::vector<uint8_t*> hd;
+    for (int s = 0; s < stripes; ++s) {
+      for (int j = 0; j < k; ++j) {
+        uint8_t* p = sl.base + sl.stride * (size_t(s) * (k + m) + j);
+        h[size_t(s * k + j) % S] ^= 0x3C;
+        CK(hipMemcpy(p, h.data(), S, hipMemcpyHostToDevice));
+        hs.push_back(p);
+      }
+      for (int r = 0; r < m; ++r) hd.push_back(sl.base + sl.stride * (size_t(s) * (k + m) + k + r));
+    }
+    const uint8_t** d_src = nullptr;
+    uint8_t** d_dst = nullptr;
+    CK(hipMalloc(&d_src, sizeof(void*) * hs.size()));
+    CK(hipMalloc(&d_dst, sizeof(void*) * hd.size()));
+    CK(hipMemcpy(d_src, hs.data(), sizeof(void*) * hs.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_dst, hd.data(), sizeof(void*) * hd.size(), hipMemcpyHostToDevice));
+    ApplyArgs& a = sl.a;
+    a.ptab = d_ptab;
+    a.src = d_src;
+    a.dst = d_dst;
+    a.nvec = int64_t(S / 16);
+    a.size = int64_t(S);
+    a.byte0 = a.nvec * 16;
+    a.src_stride = k;
+    a.dst_stride = m;
+    a.K = k;
+    a.R = m;
+    a.nt = 1;
+    slabs.push_back(sl);
+  }
+  auto launch = [&](Slab& sl) {
+    ApplyArgs args = sl.a;
+    void* kargs[] = {&args};
+    CK(hipLaunchKernel(fn, dim3(unsigned((sl.a.nvec + 255) / 256), unsigned(stripes)), dim3(256), kargs, lds, nullptr));
+  };
+  for (auto& sl : slabs) {  // host spot check of stripe 0 and the last
+    launch(sl);
+    CK(hipDeviceSynchronize());
+    std::mt19937_64 q(9);
+    for (int n = 0; n < 64; ++n) {
+      const int s = (n & 1) ? stripes - 1 : 0;
+      const size_t b = q() % S;
+      uint8_t col[k];
+      for (int j = 0; j < k; ++j)
+        CK(hipMemcpy(&col[j], sl.base + sl.stride * (size_t(s) * (k + m) + j) + b, 1, hipMemcpyDeviceToHost));
+      for (int r = 0; r < m; ++r) {
+        uint8_t e = 0, o = 0;
+        for (int j = 0; j < k; ++j) e ^= uint8_t(single_multiply(M[r * k + j], col[j], 8));
+        CK(hipMemcpy(&o, sl.base + sl.stride * (size_t(s) * (k + m) + k + r) + b, 1, hipMemcpyDeviceToHost));
+        if (o != e) {
+          std::fprintf(stderr, "skew %d: parity disagrees with the host\n", sl.skew);
+          return 1;
+        }
+      }
+    }
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int rd = 0; rd < rounds; ++rd)
+    for (auto& sl : slabs) {
+      for (int w = 0; w < 2; ++w) launch(sl);
+      for (int q = 0; q < reps; ++q) {
+        CK(hipEventRecord(e0, nullptr));
+        launch(sl);
+        CK(hipEventRecord(e1, nullptr));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        sl.t.push_back(ms * 1000.f);
+      }
+    }
+  const double bytes = double(k + m) * double(S) * stripes;
+  for (auto& sl : slabs) {
+    std::sort(sl.t.begin(), sl.t.end());
+    const double med = sl.t[sl.t.size() / 2];
+    std::printf("{\"k\": %d, \"m\": %d, \"shard_kib\": %d, \"stripes\": %d, \"skew_kib\": %d, \"median_us\": %.1f, "
+                "\"min_us\": %.1f, \"GBps\": %.0f, \"frac\": %.4f}\n",
+                k, m, kib, stripes, sl.skew, med, double(sl.t[0]), bytes / med / 1e3, bytes / med / 1e3 / 8000.0);
   }
   return 0;
 }

@@ -26,15 +26,36 @@ ECGPU_API const char* ecgpu_version(void) { return "ecgpu 0.1 (gfx950)"; }
 ECGPU_API const char* ecgpu_build_id(int what) { return what == 1 ? ECGPU_KERNEL_ID : ECGPU_BUILD_ID; }
 ECGPU_API void ecgpu_free(void* p) { std::free(p); }
 
-constexpr int64_t kShardSkew = 10240;
+// Shard-stride skew.  A lane reads the same column of every shard, so the
+// k + m concurrent accesses sit one stride apart; when that stride lines up
+// with the HBM channel / bank hash they collide.  The effect is a
+// deterministic function of the stride: an in-process sweep (RS(10,4), ~5 GiB
+// per launch, every skew's slab interleaved, tools/skew_sweep.sh) gave the same
+// numbers within ~1 % on three MI355X boxes (profiles/r03_skew_sweep_*.jsonl),
+// including sharp dips of 15-30 % (e.g. +12 KiB at 1 and 3 MiB shards, +8 KiB
+// at 2 and 6 MiB, +14 KiB at 512 KiB, no skew from 4 MiB up).  For the shard
+// sizes measured, the skew with the best worst-box rate; tie-breaks from the
+// BASELINE configs' own in-process A/Bs (RS(6,3) 1 MiB: none, 2-3 % over
+// +10 KiB; RS(10,4) 4 MiB: +14 KiB, 1.5-2 %; RS(12,4) 16 MiB: +8 KiB, 4-5 %;
+// profiles/r03_skew_ab.jsonl).  Other sizes keep +10 KiB, which is within
+// 1-4 % of the best at every size measured and never near a dip.
+struct SkewClass {
+  int64_t size, skew;
+};
+constexpr SkewClass kSkewTable[] = {
+    {256 << 10, 12 << 10}, {512 << 10, 8 << 10},  {1 << 20, 0},          {2 << 20, 12 << 10},
+    {3 << 20, 8 << 10},    {4 << 20, 14 << 10},   {6 << 20, 12 << 10},   {8 << 20, 12 << 10},
+    {12 << 20, 8 << 10},   {16 << 20, 8 << 10},   {32 << 20, 8 << 10},   {64 << 20, 8 << 10},
+};
+constexpr int64_t kDefaultSkew = 10 << 10;
 
 ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size) {
   if (size < 0) size = 0;
-  // skew = 10 KiB (an odd multiple of 2 KiB): the shard-size x skew sweep on
-  // MI355X (profiles/r01_stride_sweep.jsonl) found every
-  // power-of-two-multiple skew bad at SOME shard size (4 KiB at 1 and 3 MiB
-  // shards: -10 %; 8 KiB at 2 MiB: -15 %), 6 and 10 KiB at none
-  return ((size + 255) & ~int64_t(255)) + kShardSkew;
+  const int64_t rounded = (size + 255) & ~int64_t(255);
+  int64_t skew = kDefaultSkew;
+  for (const SkewClass& c : kSkewTable)
+    if (rounded >= c.size - c.size / 16 && rounded <= c.size + c.size / 16) skew = c.skew;
+  return rounded + skew;
 }
 
 ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w) { return single_multiply(a, b, w); }

@@ -139,8 +139,16 @@ def test_decode_plan_replays_reference_decode(golden, vectors):
 
 def test_recommended_stride():
     from erasure_coding_test_amd import _native as N
-    assert N.lib.ecgpu_recommended_shard_stride(4 << 20) == (4 << 20) + 10240
-    assert N.lib.ecgpu_recommended_shard_stride(1) % 256 == 0
+    # per-size skew table (capi_host.cpp kSkewTable, profiles/r03_skew_sweep_*.jsonl), +10 KiB elsewhere
+    st = N.lib.ecgpu_recommended_shard_stride
+    assert st(4 << 20) == (4 << 20) + (14 << 10)
+    assert st((4 << 20) + 3) == (4 << 20) + 256 + (14 << 10)
+    assert st(16 << 20) == (16 << 20) + (8 << 10)
+    assert st(1 << 20) == 1 << 20
+    assert st(5 << 20) == (5 << 20) + (10 << 10)
+    assert st(349525) == ((349525 + 255) & ~255) + (10 << 10)  # ECX block size
+    for size in (1, 7, 4095, 65536, (1 << 20) - 1, (3 << 20) + 17, 100 << 20):
+        assert st(size) % 256 == 0 and st(size) >= size
 
 
 NO_GPU = not os.path.exists("/dev/kfd")

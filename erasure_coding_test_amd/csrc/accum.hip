@@ -162,7 +162,7 @@ ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int
   }
   a->pending = true;
   const FusedOp op = accum_op(a, src, coefs);
-  if (inline_ok(op)) {
+  if (inline_ok(op, a->size)) {
     add_stats(op);
     std::vector<const uint8_t*> sp;
     for (void* p : op.srcs) sp.push_back(static_cast<const uint8_t*>(p));

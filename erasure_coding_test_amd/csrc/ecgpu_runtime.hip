@@ -699,10 +699,7 @@ bool zero_copy_pinned() {
   return v;
 }
 
-bool inline_enabled() {
-  static const bool v = env_int("ECGPU_INLINE", 1) != 0;
-  return v;
-}
+bool inline_enabled() { return env_int("ECGPU_INLINE", 1) != 0; }  // per call (A/B in one process)
 
 int ensure_bounce(Ctx* c, size_t bytes) {
   if (bytes <= c->bounce_cap) return ECGPU_OK;
@@ -867,9 +864,17 @@ void build_p3(uint32_t c, uint32_t* p3) {
 // arguments, no table or pointer upload)?  w = 8, 1..16 sources, the
 // production engine, and no output that is also a source when the rows need
 // more than one launch.
-bool inline_ok(const FusedOp& op) {
+bool inline_ok(const FusedOp& op, int64_t size) {
   const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
-  return inline_enabled() && op.w == 8 && nsrc >= 1 && nsrc <= dev::kMaxSpecK && rows >= 1 &&
+  // The inline kernels with 15-16 sources and a full 4-row launch hold more
+  // coefficient tables than the SGPR file and spill them to VGPR lanes (the
+  // plan kernel loads them as it goes): a dense RS(16,4) 64 MiB encode ran
+  // 574 us inline against 229 us as a plan launch (tools/probe_inline.py,
+  // profiles/r03_inline_vs_plan.csv); K = 14 and below are equal.  Large
+  // such calls take the plan; small ones stay inline, where the table upload
+  // a plan needs would cost more than the spills.
+  const bool spills = nsrc >= 15 && rows >= dev::kMaxRows && size > (int64_t(1) << 20);
+  return inline_enabled() && op.w == 8 && nsrc >= 1 && nsrc <= dev::kMaxSpecK && rows >= 1 && !spills &&
          env_int("ECGPU_KERNEL", ECGPU_KERNEL_PERM) == ECGPU_KERNEL_PERM && !(op.dst_is_src && rows > dev::kMaxRows);
 }
 
@@ -1154,7 +1159,7 @@ int execute(const FusedOp& op, int64_t size) {
   if (!lease.c) return lease.rc;
   Ctx* c = lease.c;
   DeviceGuard g(device);
-  const bool inl = inline_ok(op);
+  const bool inl = inline_ok(op, size);
   CallMap m;
   if (int rc = map_buffers(op, size, device, inl, &m)) return rc;
   if (inl && m.nstage > 0 && m.nstage * size_t(size) <= zc_max()) return exec_zero_copy(c, op, m);

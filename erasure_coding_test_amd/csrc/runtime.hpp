@@ -140,7 +140,7 @@ int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>&
 
 // ---- synchronous execution ----------------------------------------------------
 void add_stats(const FusedOp& op);
-bool inline_ok(const FusedOp& op);
+bool inline_ok(const FusedOp& op, int64_t size);
 int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, const std::vector<uint8_t*>& dp,
                   int64_t size, hipStream_t s, bool host_io);
 int execute(const FusedOp& op, int64_t size);

@@ -1400,3 +1400,28 @@ def test_maximum_int_size_roundtrip(ec, gpu, k, m, erasures):
     torch.cuda.synchronize()
     for e, want in keep.items():
         assert torch.equal((dd + dc)[e], want), e
+
+
+@pytest.mark.parametrize("k", [15, 16])
+@pytest.mark.parametrize("size", [(1 << 20) - 48, (2 << 20) + 16])
+def test_dense_wide_k_calls_inline_or_plan(ec, gpu, restatement, k, size):
+    """Calls with 15-16 sources and 4+ dense rows run inline up to 1 MiB and
+    as a plan launch above (inline_ok: those inline kernels spill their
+    tables); both sides of the switch, device buffers and pageable host
+    buffers, against the oracle."""
+    import torch
+    m = 5  # a full 4-row launch plus one more
+    rng = np.random.default_rng(k * 1000 + size % 997)
+    M = [int(x) for x in rng.integers(2, 256, k * m)]
+    data = host_shards(80, k, k, size)
+    ref = _encode_ref(restatement, k, m, M, data, size)
+    dd = to_dev([d[:size] for d in data], gpu)
+    dc = [torch.zeros(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, dd, dc, size)
+    torch.cuda.synchronize()
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), ref[i][:size]), i
+    hc = alloc_shards(m, size, PAD)
+    ec.jerasure.jerasure_matrix_encode(k, m, 8, M, data, hc, size)
+    for i in range(m):
+        assert np.array_equal(hc[i][:size], ref[i][:size]), i

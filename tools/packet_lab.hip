@@ -79,12 +79,118 @@ __global__ __launch_bounds__(kBlock) void packets16p_r2(PacketArgs a) {
   for (int r = 0; r < RT; ++r)
     if (r < a.R) store16t<1>(a.dst[r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
 }
+// Output rows split across the waves of a workgroup: SPLIT waves share one
+// 64-column block and each keeps RT = 32 / SPLIT rows, so a wave holds
+// 4·RT accumulator VGPRs instead of 128 (more waves resident per SIMD); the
+// SPLIT waves read the same source lines, the later ones from cache.  NT
+// selects non-temporal source loads.
+template <int RT, int SPLIT, int NT>
+__global__ __launch_bounds__(kBlock) void packets16p_split(PacketArgs a) {
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int half = wave % SPLIT;
+  const int64_t g = int64_t(blockIdx.x) * (kBlock / SPLIT) + (wave / SPLIT) * 64 + (threadIdx.x & 63);
+  if (g >= a.ncols) return;
+  int64_t sp, col;
+  packet_coords(a, g, &sp, &col);
+  const int64_t soff = sp * a.sstride + col * 16, doff = sp * a.dstride + col * 16;
+  uint32_t acc[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+  const int nc = a.nsrc >> 2;
+  const int shift = half * RT;
+  u32x4 xa[4], xb[4];
+  uint32_t ma[4], mb[4];
+  auto load4 = [&](u32x4 (&x)[4], uint32_t (&m)[4], int c) {
+    const int b = (c < nc ? c : nc - 1) * 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      m[u] = a.mask[b + u] >> shift;
+      x[u] = load16t<NT>(a.src[b + u] + soff, 0);
+    }
+  };
+  auto apply4 = [&](const u32x4 (&x)[4], const uint32_t (&m)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xor_masked16<RT, 4>(acc, x[u], m[u]);
+  };
+  if (nc > 0) {
+    load4(xa, ma, 0);
+    for (int c = 0; c < nc; c += 2) {
+      load4(xb, mb, c + 1);
+      apply4(xa, ma);
+      if (c + 1 >= nc) break;
+      load4(xa, ma, c + 2);
+      apply4(xb, mb);
+    }
+  }
+  for (int j = nc * 4; j < a.nsrc; ++j) xor_masked16<RT, 4>(acc, load16t<NT>(a.src[j] + soff, 0), a.mask[j] >> shift);
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+    if (shift + r < a.R) store16t<1>(a.dst[shift + r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+}
+// Timing probe, wrong output: the production loop with the masked XOR on
+// dwords 2-3 replaced by a single unmasked XOR per source, i.e. ~half the
+// VALU work for the same loads and stores -- measures how VALU-bound the
+// production kernel is.
+template <int RT>
+__device__ __forceinline__ void xor_masked16_half(uint32_t (&acc)[RT][4], const u32x4& x, uint32_t m) {
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    const uint32_t sel = uint32_t(int32_t(m << (31 - r)) >> 31);
+    acc[r][0] = __builtin_amdgcn_bitop3_b32(acc[r][0], x[0], sel, 0x78);
+    acc[r][1] = __builtin_amdgcn_bitop3_b32(acc[r][1], x[1], sel, 0x78);
+  }
+  acc[0][2] ^= x[2];
+  acc[0][3] ^= x[3];
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int RT>
+__global__ __launch_bounds__(kBlock) void packets16p_halfvalu(PacketArgs a) {
+  const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= a.ncols) return;
+  int64_t sp, col;
+  packet_coords(a, g, &sp, &col);
+  const int64_t soff = sp * a.sstride + col * 16, doff = sp * a.dstride + col * 16;
+  uint32_t acc[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+  const int nc = a.nsrc >> 2;
+  u32x4 xa[4], xb[4];
+  uint32_t ma[4], mb[4];
+  auto load4 = [&](u32x4 (&x)[4], uint32_t (&m)[4], int c) {
+    const int b = (c < nc ? c : nc - 1) * 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      m[u] = a.mask[b + u];
+      x[u] = load16t<1>(a.src[b + u] + soff, 0);
+    }
+  };
+  auto apply4 = [&](const u32x4 (&x)[4], const uint32_t (&m)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xor_masked16_half<RT>(acc, x[u], m[u]);
+  };
+  if (nc > 0) {
+    load4(xa, ma, 0);
+    for (int c = 0; c < nc; c += 2) {
+      load4(xb, mb, c + 1);
+      apply4(xa, ma);
+      if (c + 1 >= nc) break;
+      load4(xa, ma, c + 2);
+      apply4(xb, mb);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+    if (r < a.R) store16t<1>(a.dst[r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+}
 }  // namespace lab
 
 struct Variant {
   std::string name;
   const void* fn;
   unsigned lds = 0;  // dynamic LDS per workgroup: an unused allocation that caps residency
+  int split = 1;     // waves sharing one column block (grid scales by it)
+  bool check = true; // false: a timing probe whose output is deliberately wrong
 };
 
 int main(int argc, char** argv) {
@@ -150,13 +256,14 @@ int main(int argc, char** argv) {
   int dev = 0, lds_cu = 0;
   CK(hipGetDevice(&dev));
   CK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
-  for (int b : {1, 2})
-    vs.push_back({"prod_packets16p_cap" + std::to_string(b), reinterpret_cast<const void*>(&gf_xor_packets16p<32>),
-                  unsigned(lds_cu / b) & ~511u});
+  vs.push_back({"split2_nt", reinterpret_cast<const void*>(&lab::packets16p_split<16, 2, 1>), 0, 2});
+  vs.push_back({"probe_half_valu", reinterpret_cast<const void*>(&lab::packets16p_halfvalu<32>), 0, 1, false});
+  (void)lds_cu;
   auto launch = [&](const Variant& v) {
     PacketArgs args = a;
     void* kargs[] = {&args};
-    CK(hipLaunchKernel(v.fn, dim3(unsigned((a.ncols + kBlock - 1) / kBlock)), dim3(kBlock), kargs, v.lds, nullptr));
+    const int64_t per = kBlock / v.split;
+    CK(hipLaunchKernel(v.fn, dim3(unsigned((a.ncols + per - 1) / per)), dim3(kBlock), kargs, v.lds, nullptr));
   };
   launch(vs[0]);
   CK(hipDeviceSynchronize());
@@ -183,6 +290,7 @@ int main(int argc, char** argv) {
     }
   }
   for (size_t v = 1; v < vs.size(); ++v) {
+    if (!vs[v].check) continue;
     CK(hipMemset(slab + stride * size_t(k), 0, stride * size_t(m)));
     launch(vs[v]);
     CK(hipDeviceSynchronize());

@@ -61,13 +61,21 @@ ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size) {
 ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w) { return single_multiply(a, b, w); }
 ECGPU_API int ecgpu_galois_single_divide(int a, int b, int w) { return single_divide(a, b, w); }
 ECGPU_API int ecgpu_galois_inverse(int a, int w) { return inverse(a, w); }
+// Log / antilog lookups (galois.cpp:269-289).  The reference indexes its
+// tables unchecked; here a value outside them -- log: [0, 2^w), ilog:
+// [-(2^w - 1), 2(2^w - 1)), the offset table the divide path uses -- or a w
+// without tables (w > 30, where the reference exits) returns -1.
 ECGPU_API int ecgpu_galois_log(int value, int w) {
   int* t = log_table(w);
-  return t ? t[value] : -1;
+  if (!t || value < 0 || int64_t(value) >= (int64_t(1) << w)) return -1;
+  return t[value];
 }
 ECGPU_API int ecgpu_galois_ilog(int value, int w) {
   int* t = ilog_table(w);
-  return t ? t[value] : -1;
+  if (!t) return -1;
+  const int64_t nwm1 = (int64_t(1) << w) - 1;
+  if (value < -nwm1 || value >= 2 * nwm1) return -1;
+  return t[value];
 }
 
 ECGPU_API int* ecgpu_reed_sol_vandermonde_coding_matrix(int k, int m, int w) {

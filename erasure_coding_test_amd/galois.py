@@ -1,6 +1,8 @@
 """galois.h surface (reference include/galois.h:41-95) over the C ABI.
 
-Scalar field ops run on the host; the w=8 region ops run on the MI355X.
+Scalar field ops run on the host (csrc/gf_host.cpp); the region ops run on
+the MI355X.  Where the reference prints an error and exits (log tables for
+w > 30) the mirror raises ValueError.
 """
 from __future__ import annotations
 
@@ -9,22 +11,39 @@ from ._buffers import addr
 
 
 def galois_single_multiply(a: int, b: int, w: int) -> int:
+    """a * b in GF(2^w) (galois.cpp:322-360)."""
     return N.lib.ecgpu_galois_single_multiply(a, b, w)
 
 
 def galois_single_divide(a: int, b: int, w: int) -> int:
+    """a / b in GF(2^w); -1 for b = 0 (galois.cpp:367-398)."""
     return N.lib.ecgpu_galois_single_divide(a, b, w)
 
 
 def galois_inverse(a: int, w: int) -> int:
+    """1 / a in GF(2^w); -1 for a = 0 (galois.cpp:597-603)."""
     return N.lib.ecgpu_galois_inverse(a, w)
 
 
+def _log_width(fn: str, w: int) -> None:
+    if not 1 <= w <= 30:  # galois.cpp:273-274, 284-285: "w is too big", exit(1)
+        raise ValueError(f"{fn}: w = {w} has no log tables (w <= 30)")
+
+
 def galois_log(value: int, w: int) -> int:
+    """Discrete log of value, 0 <= value < 2^w (galois.cpp:280-289)."""
+    _log_width("galois_log", w)
+    if not 0 <= value < (1 << w):
+        raise ValueError(f"galois_log: value {value} outside [0, 2^{w})")
     return N.lib.ecgpu_galois_log(value, w)
 
 
 def galois_ilog(value: int, w: int) -> int:
+    """Antilog, -(2^w - 1) <= value < 2(2^w - 1) like the reference's offset table (galois.cpp:269-278)."""
+    _log_width("galois_ilog", w)
+    nwm1 = (1 << w) - 1
+    if not -nwm1 <= value < 2 * nwm1:
+        raise ValueError(f"galois_ilog: value {value} outside [-{nwm1}, {2 * nwm1})")
     return N.lib.ecgpu_galois_ilog(value, w)
 
 

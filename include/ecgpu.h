@@ -64,6 +64,8 @@ ECGPU_API void ecgpu_free(void* p);                    /* == free()           */
 ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w); /* galois.cpp:322-360 */
 ECGPU_API int ecgpu_galois_single_divide(int a, int b, int w);   /* galois.cpp:367-398 */
 ECGPU_API int ecgpu_galois_inverse(int a, int w);                /* galois.cpp:597-603 */
+/* log: value in [0, 2^w); ilog: value in [-(2^w - 1), 2(2^w - 1)).  -1 for a
+ * value outside the table or w > 30 (the reference reads out of bounds / exits) */
 ECGPU_API int ecgpu_galois_log(int value, int w);                /* galois.cpp:280-289 */
 ECGPU_API int ecgpu_galois_ilog(int value, int w);               /* galois.cpp:269-278 */
 

@@ -1402,6 +1402,52 @@ def test_maximum_int_size_roundtrip(ec, gpu, k, m, erasures):
         assert torch.equal((dd + dc)[e], want), e
 
 
+@pytest.mark.parametrize("w", [16, 32])
+def test_maximum_int_size_wide_words(ec, gpu, w):
+    """w = 16 / 32 at the largest `int size` the word size allows (2^31 - 4:
+    134M 16-B columns through the LDS nibble kernels plus a 12-byte tail):
+    RS(2,1)'s parity row is all ones, so the parity must equal the torch XOR
+    of the data; then RS(2,1) decode of data shard 0 restores it."""
+    import torch
+    k, m, size = 2, 1, 2**31 - 4
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w)
+    g = torch.Generator(device=gpu).manual_seed(w)
+    dd = [torch.randint(0, 256, (size,), dtype=torch.uint8, device=gpu, generator=g) for _ in range(k)]
+    dc = [torch.empty(size, dtype=torch.uint8, device=gpu)]
+    ec.jerasure.jerasure_matrix_encode(k, m, w, M, dd, dc, size)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.bitwise_xor(dd[0], dd[1]), dc[0])
+    keep = dd[0].clone()
+    dd[0].fill_(0)
+    assert ec.jerasure.jerasure_matrix_decode(k, m, w, M, 0, [0], dd, dc, size) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dd[0], keep)
+
+
+def test_maximum_int_size_bitmatrix(ec, gpu):
+    """Bit-matrix packet coding at the largest `int size` that is whole
+    super-packets for w = 8, packetsize 8 KiB (2^31 - 64 KiB; 16.8M packet
+    columns of 16 B): RS(2,1)'s bit-matrix is two identity blocks, so every
+    parity packet row is the XOR of the data rows -- the torch XOR of the
+    shards -- and the bit-matrix decode of data shard 0 restores it."""
+    import torch
+    k, m, w, ps = 2, 1, 8, 8192
+    size = 2**31 - w * ps
+    J = ec.jerasure
+    bm = J.jerasure_matrix_to_bitmatrix(k, m, w, ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w))
+    g = torch.Generator(device=gpu).manual_seed(3)
+    dd = [torch.randint(0, 256, (size,), dtype=torch.uint8, device=gpu, generator=g) for _ in range(k)]
+    dc = [torch.empty(size, dtype=torch.uint8, device=gpu)]
+    J.jerasure_bitmatrix_encode(k, m, w, bm, dd, dc, size, ps)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.bitwise_xor(dd[0], dd[1]), dc[0])
+    keep = dd[0].clone()
+    dd[0].fill_(0)
+    assert J.jerasure_bitmatrix_decode(k, m, w, bm, 0, [0], dd, dc, size, ps) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dd[0], keep)
+
+
 @pytest.mark.parametrize("k", [15, 16])
 @pytest.mark.parametrize("size", [(1 << 20) - 48, (2 << 20) + 16])
 def test_dense_wide_k_calls_inline_or_plan(ec, gpu, restatement, k, size):

@@ -43,6 +43,28 @@ def test_scalar_field_matches_reference(golden, vectors):
             assert galois.galois_single_multiply(q, b, 8) == a
 
 
+def test_log_tables_out_of_range():
+    """The reference indexes its log tables unchecked and exits for w > 30
+    (galois.cpp:269-289): the C ABI returns -1 there, the mirror raises."""
+    from erasure_coding_test_amd import _native as N
+    for w in (4, 8, 16):
+        nwm1 = (1 << w) - 1
+        assert N.lib.ecgpu_galois_log(nwm1, w) == galois.galois_log(nwm1, w) >= 0
+        assert N.lib.ecgpu_galois_ilog(-nwm1, w) == galois.galois_ilog(-nwm1, w) == 1
+        assert N.lib.ecgpu_galois_ilog(2 * nwm1 - 1, w) == galois.galois_ilog(2 * nwm1 - 1, w) >= 1
+        for bad in (-1, nwm1 + 1, 1 << 30):
+            assert N.lib.ecgpu_galois_log(bad, w) == -1
+            with pytest.raises(ValueError):
+                galois.galois_log(bad, w)
+        for bad in (-nwm1 - 1, 2 * nwm1):
+            assert N.lib.ecgpu_galois_ilog(bad, w) == -1
+            with pytest.raises(ValueError):
+                galois.galois_ilog(bad, w)
+    assert N.lib.ecgpu_galois_log(1, 32) == -1
+    with pytest.raises(ValueError):
+        galois.galois_log(1, 31)
+
+
 @pytest.mark.parametrize("w", [4, 8, 16, 32])
 def test_field_axioms_other_widths(w):
     import random

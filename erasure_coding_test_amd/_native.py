@@ -46,6 +46,14 @@ SIGNATURES = {
     "ecgpu_galois_inverse": (c_int, [c_int, c_int]),
     "ecgpu_galois_log": (c_int, [c_int, c_int]),
     "ecgpu_galois_ilog": (c_int, [c_int, c_int]),
+    "ecgpu_galois_create_log_tables": (c_int, [c_int]),
+    "ecgpu_galois_create_mult_tables": (c_int, [c_int]),
+    "ecgpu_galois_get_mult_table": (c_int_p, [c_int]),
+    "ecgpu_galois_get_div_table": (c_int_p, [c_int]),
+    "ecgpu_galois_get_log_table": (c_int_p, [c_int]),
+    "ecgpu_galois_get_ilog_table": (c_int_p, [c_int]),
+    "ecgpu_galois_shift_multiply": (c_int, [c_int, c_int, c_int]),
+    "ecgpu_galois_shift_inverse": (c_int, [c_int, c_int]),
     "ecgpu_reed_sol_vandermonde_coding_matrix": (c_void_p, [c_int, c_int, c_int]),
     "ecgpu_reed_sol_extended_vandermonde_matrix": (c_void_p, [c_int, c_int, c_int]),
     "ecgpu_reed_sol_big_vandermonde_distribution_matrix": (c_void_p, [c_int, c_int, c_int]),

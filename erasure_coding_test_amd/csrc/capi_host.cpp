@@ -70,6 +70,19 @@ ECGPU_API int ecgpu_galois_log(int value, int w) {
   if (!t || value < 0 || int64_t(value) >= (int64_t(1) << w)) return -1;
   return t[value];
 }
+// Table construction / access and the table-free shift arithmetic
+// (galois.cpp:152-267, :292-320, :605-665, galois.h:46-66).  Tables are
+// built once per w, thread-safely, and live for the library's lifetime; a
+// w the reference cannot build tables for gives -1 / NULL.
+ECGPU_API int ecgpu_galois_create_log_tables(int w) { return create_log_tables(w); }
+ECGPU_API int ecgpu_galois_create_mult_tables(int w) { return create_mult_tables(w); }
+ECGPU_API int* ecgpu_galois_get_mult_table(int w) { return mult_table(w); }
+ECGPU_API int* ecgpu_galois_get_div_table(int w) { return div_table(w); }
+ECGPU_API int* ecgpu_galois_get_log_table(int w) { return log_table(w); }
+ECGPU_API int* ecgpu_galois_get_ilog_table(int w) { return ilog_table(w); }
+ECGPU_API int ecgpu_galois_shift_multiply(int a, int b, int w) { return shift_multiply(a, b, w); }
+ECGPU_API int ecgpu_galois_shift_inverse(int a, int w) { return shift_inverse(a, w); }
+
 ECGPU_API int ecgpu_galois_ilog(int value, int w) {
   int* t = ilog_table(w);
   if (!t) return -1;

@@ -254,3 +254,54 @@ class ScheduleCache:
             self.close()
         except Exception:
             pass
+
+
+# The reference's names for the schedule-cache and schedule lifetime calls
+# (jerasure.h:116-119, :185).  Schedules here are Python lists, so freeing one is a
+# no-op; a cache owns C memory and is released by jerasure_free_schedule_cache
+# (or when it is garbage-collected).
+def jerasure_generate_schedule_cache(k: int, m: int, w: int, bitmatrix, smart: int) -> Optional[ScheduleCache]:
+    """jerasure.cpp:997-1032: None (the reference's NULL) unless m == 2."""
+    try:
+        return ScheduleCache(k, m, w, bitmatrix, smart)
+    except ValueError:
+        return None
+
+
+def jerasure_schedule_decode_cache(k: int, m: int, w: int, scache: ScheduleCache, erasures, data_ptrs, coding_ptrs,
+                                   size: int, packetsize: int) -> int:
+    """jerasure.cpp:963-995 with a cache from jerasure_generate_schedule_cache."""
+    if (scache.k, scache.m, scache.w) != (k, m, w):
+        raise ValueError("jerasure_schedule_decode_cache: cache was built for another (k, m, w)")
+    return scache.decode(erasures, data_ptrs, coding_ptrs, size, packetsize)
+
+
+def jerasure_free_schedule_cache(k: int, m: int, cache: Optional[ScheduleCache]) -> None:
+    """jerasure.cpp:543-560."""
+    if cache is not None:
+        cache.close()
+
+
+def jerasure_free_schedule(schedule) -> None:
+    """jerasure.cpp:534-541: schedules are Python lists here; nothing to free."""
+
+
+def jerasure_print_matrix(matrix, rows: int, cols: int, w: int, file=None) -> None:
+    """jerasure.cpp:46-68: entries as unsigned ints right-aligned to the width
+    of 2^w - 1 (10 for w = 32), one row per line."""
+    import sys
+    out = file or sys.stdout
+    fw = 10 if w == 32 else len(str((1 << w) - 1))
+    for i in range(rows):
+        out.write(" ".join(f"{matrix[i * cols + j] & 0xFFFFFFFF:>{fw}}" for j in range(cols)) + "\n")
+
+
+def jerasure_print_bitmatrix(bitmatrix, rows: int, cols: int, w: int, file=None) -> None:
+    """jerasure.cpp:70-82: w x w blocks, a space between block columns and an
+    empty line between block rows."""
+    import sys
+    out = file or sys.stdout
+    for i in range(rows):
+        if i and i % w == 0:
+            out.write("\n")
+        out.write("".join((" " if j and j % w == 0 else "") + str(bitmatrix[i * cols + j]) for j in range(cols)) + "\n")

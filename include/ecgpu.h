@@ -68,6 +68,19 @@ ECGPU_API int ecgpu_galois_inverse(int a, int w);                /* galois.cpp:5
  * value outside the table or w > 30 (the reference reads out of bounds / exits) */
 ECGPU_API int ecgpu_galois_log(int value, int w);                /* galois.cpp:280-289 */
 ECGPU_API int ecgpu_galois_ilog(int value, int w);               /* galois.cpp:269-278 */
+/* Field tables, built once per w and kept for the library's lifetime
+ * (galois.cpp:627-665, galois.h:46-66): 0 / -1 like galois_create_*_tables, NULL where the
+ * reference cannot build them.  mult / div: 2^(2w) entries indexed (x << w) | y
+ * (w <= 13); log: 2^w entries; ilog: offset pointer valid on
+ * [-(2^w - 1), 2(2^w - 1)) (w <= 30). */
+ECGPU_API int ecgpu_galois_create_log_tables(int w);             /* galois.cpp:152-191 */
+ECGPU_API int ecgpu_galois_create_mult_tables(int w);            /* galois.cpp:218-267 */
+ECGPU_API int* ecgpu_galois_get_mult_table(int w);
+ECGPU_API int* ecgpu_galois_get_div_table(int w);
+ECGPU_API int* ecgpu_galois_get_log_table(int w);
+ECGPU_API int* ecgpu_galois_get_ilog_table(int w);
+ECGPU_API int ecgpu_galois_shift_multiply(int a, int b, int w);  /* galois.cpp:292-320 */
+ECGPU_API int ecgpu_galois_shift_inverse(int a, int w);          /* galois.cpp:605-625 */
 
 /* ------------------------------------------- matrices (host only) ------- */
 ECGPU_API int* ecgpu_reed_sol_vandermonde_coding_matrix(int k, int m, int w);            /* reed_sol.cpp:63-84   */

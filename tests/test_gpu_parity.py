@@ -1216,7 +1216,7 @@ def test_schedule_decode_lazy_and_cache_device(ec, gpu, smart):
     coding = [torch.zeros(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
     J.jerasure_schedule_encode(k, m, w, J.jerasure_smart_bitmatrix_to_schedule(k, m, w, bm), data, coding, size, ps)
     orig = [t.clone() for t in data + coding]
-    cache = J.ScheduleCache(k, m, w, bm, smart)
+    cache = J.jerasure_generate_schedule_cache(k, m, w, bm, smart)
     for er in ([0], [k], [1, 4], [2, k + 1], [k, k + 1]):
         for method in ("lazy", "cache"):
             for e in er:
@@ -1224,12 +1224,12 @@ def test_schedule_decode_lazy_and_cache_device(ec, gpu, smart):
             if method == "lazy":
                 assert J.jerasure_schedule_decode_lazy(k, m, w, bm, er, data, coding, size, ps, smart) == 0
             else:
-                assert cache.decode(er, data, coding, size, ps) == 0
+                assert J.jerasure_schedule_decode_cache(k, m, w, cache, er, data, coding, size, ps) == 0
             torch.cuda.synchronize()
             for i, t in enumerate(data + coding):
                 assert torch.equal(t, orig[i]), (er, method, i)
-    assert cache.decode([0, 1, 2], data, coding, size, ps) == -1
-    cache.close()
+    assert J.jerasure_schedule_decode_cache(k, m, w, cache, [0, 1, 2], data, coding, size, ps) == -1
+    J.jerasure_free_schedule_cache(k, m, cache)
 
 
 # ------------------------------------------- randomized (seeded) cases ----

@@ -9,12 +9,12 @@ Each case draws one of
     last may be undecodable: the return code must match), row_k_ones 0/1;
   * galois_w08_region_multiply with and without add, galois_region_xor;
   * jerasure_matrix_dotprod with and without src_ids,
-with sizes from 8 B to 640 KiB in whole 8-byte words (the reference's loops
+with sizes from 8 B to 2 MiB in whole 8-byte words (the reference's loops
 over-run other sizes by design, galois.cpp:452-465), on device tensors,
 pageable numpy arrays or pinned tensors -- so every staging mode of a
 synchronous call (device, zero-copy, bounce, outputs in coherent memory,
 HIP copies, pinned in place) is crossed with every shape class.
-ECGPU_FUZZ_CASES sets the case count (default 1500, ~10 s on MI355X).
+ECGPU_FUZZ_CASES sets the case count (default 1500, ~15 s on MI355X).
 """
 import os
 
@@ -30,7 +30,9 @@ def ec(gpu):
     return E
 
 
-SIZES = [8, 24, 4096, 4104, 65536, 100000, 262144, 349528, 655360]
+# 1 MiB + 8 and 2 MiB + 16 cross inline_ok's switch for 15-16 dense sources
+# (inline up to 1 MiB, plan launches above)
+SIZES = [8, 24, 4096, 4104, 65536, 100000, 262144, 349528, 655360, (1 << 20) + 8, (2 << 20) + 16]
 
 
 def _bufs(arrays, where, gpu):
@@ -55,7 +57,7 @@ def test_fuzz_sync_calls_vs_reference(ec, gpu, reference):
         kind = ("encode", "decode", "region", "dotprod")[int(rng.integers(0, 4))]
         where = ("device", "pageable", "pinned")[int(rng.integers(0, 3))]
         size = int(rng.choice(SIZES))
-        if size > 100000 and rng.random() < 0.5:
+        if 100000 < size < (1 << 20) and rng.random() < 0.5:
             size = 8 * int(rng.integers(1, size // 8))  # ragged within the range, still whole words
         ctx = (case, kind, where, size)
         kinds[kind] += 1

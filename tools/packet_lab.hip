@@ -18,6 +18,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "gf_host.hpp"
@@ -127,6 +128,62 @@ __global__ __launch_bounds__(kBlock) void packets16p_split(PacketArgs a) {
   for (int r = 0; r < RT; ++r)
     if (shift + r < a.R) store16t<1>(a.dst[shift + r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
 }
+// Deeper source pipeline: chunks of CH source rows in NB rotating buffers, so
+// (NB - 1) * CH + CH loads of 1 KiB per wave can be in flight (production: 2
+// buffers of 4).  More VGPRs (2 waves per SIMD instead of 3) for more bytes
+// in flight per SIMD.  Chunk indices past the last full chunk re-read it.
+template <int RT, int CH, int NB>
+__global__ __launch_bounds__(kBlock) void packets16_ring(PacketArgs a) {
+  static_assert(NB == 2 || NB == 3, "ring of 2 or 3 chunk buffers");
+  const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= a.ncols) return;
+  int64_t sp, col;
+  packet_coords(a, g, &sp, &col);
+  const int64_t soff = sp * a.sstride + col * 16, doff = sp * a.dstride + col * 16;
+  uint32_t acc[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+  const int nc = a.nsrc / CH;
+  u32x4 x[NB][CH];
+  uint32_t msk[NB][CH];
+  // buffer indices are template constants so the ring stays in registers
+  auto load = [&](auto bc, int c) {
+    constexpr int b = decltype(bc)::value;
+    const int base = (c < nc ? c : nc - 1) * CH;
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      msk[b][u] = a.mask[base + u];
+      x[b][u] = load16t<1>(a.src[base + u] + soff, 0);
+    }
+  };
+  auto apply = [&](auto bc) {
+    constexpr int b = decltype(bc)::value;
+#pragma unroll
+    for (int u = 0; u < CH; ++u) xor_masked16<RT, 4>(acc, x[b][u], msk[b][u]);
+  };
+  auto step = [&](auto bc, int c) -> bool {  // false: past the last chunk
+    constexpr int b = decltype(bc)::value;
+    load(std::integral_constant<int, (b + NB - 1) % NB>{}, c + b + NB - 1);
+    if (c + b >= nc) return false;
+    apply(bc);
+    return true;
+  };
+  if (nc > 0) {
+    load(std::integral_constant<int, 0>{}, 0);
+    if constexpr (NB > 2) load(std::integral_constant<int, 1>{}, 1);
+    for (int c = 0; c < nc; c += NB) {
+      if (!step(std::integral_constant<int, 0>{}, c)) break;
+      if (!step(std::integral_constant<int, 1>{}, c)) break;
+      if constexpr (NB > 2)
+        if (!step(std::integral_constant<int, 2>{}, c)) break;
+    }
+  }
+  for (int j = nc * CH; j < a.nsrc; ++j) xor_masked16<RT, 4>(acc, load16t<1>(a.src[j] + soff, 0), a.mask[j]);
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+    if (r < a.R) store16t<1>(a.dst[r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+}
+
 // Timing probe, wrong output: the production loop with the masked XOR on
 // dwords 2-3 replaced by a single unmasked XOR per source, i.e. ~half the
 // VALU work for the same loads and stores -- measures how VALU-bound the
@@ -256,8 +313,11 @@ int main(int argc, char** argv) {
   int dev = 0, lds_cu = 0;
   CK(hipGetDevice(&dev));
   CK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
-  vs.push_back({"split2_nt", reinterpret_cast<const void*>(&lab::packets16p_split<16, 2, 1>), 0, 2});
-  vs.push_back({"probe_half_valu", reinterpret_cast<const void*>(&lab::packets16p_halfvalu<32>), 0, 1, false});
+  vs.push_back({"ring_c4x2", reinterpret_cast<const void*>(&lab::packets16_ring<32, 4, 2>)});
+  vs.push_back({"ring_c4x3", reinterpret_cast<const void*>(&lab::packets16_ring<32, 4, 3>)});
+  vs.push_back({"ring_c8x2", reinterpret_cast<const void*>(&lab::packets16_ring<32, 8, 2>)});
+  vs.push_back({"ring_c8x3", reinterpret_cast<const void*>(&lab::packets16_ring<32, 8, 3>)});
+  vs.push_back({"ring_c6x3", reinterpret_cast<const void*>(&lab::packets16_ring<32, 6, 3>)});
   (void)lds_cu;
   auto launch = [&](const Variant& v) {
     PacketArgs args = a;

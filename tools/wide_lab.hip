@@ -5,7 +5,7 @@
 // sample columns), then timed in interleaved rounds with HIP events.
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I erasure_coding_test_amd/csrc \
-//     tools/wide_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp -o tools/wide_lab.bin
+//     tools/wide_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp erasure_coding_test_amd/csrc/matrix_host.cpp -o tools/wide_lab.bin
 //   tools/wide_lab.bin [--w 32] [--k 10] [--m 4] [--mib 64] [--rounds 7] [--reps 10] [--only name]
 //
 // Prints one JSON line per variant: median / min us and GB/s of (k+m)*S.
@@ -249,6 +249,104 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   }
 }
 
+// w = 16 with the unit structure of gf_apply_wide_nib<R, 1>: the launch's row
+// 0 and column 0 are all ones, so row 0 is the XOR of the sources and source
+// 0 is XORed into every row; the LDS holds the packed pairs of rows
+// 1..R-1 (pair p = rows 1 + 2p, 2 + 2p) for sources 1..K-1 only.
+template <int R, int CHUNK, int GROUPS>
+__global__ __launch_bounds__(kBlock) void nib16u(ApplyArgs a) {
+  constexpr int L = R - 1;
+  constexpr int EW = nib16_entry_words(L), EB = 4 * EW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int K = a.K;
+  const int n = (K - 1) * kNibWords * EW;
+  for (int i = threadIdx.x; i < n; i += kBlock) {
+    const int pr = i % EW, e = (i / EW) % kNibWords, j = i / (EW * kNibWords) + 1;
+    const bool high = (e >> 4) >= 4;
+    auto word = [&](int r) -> uint32_t {
+      if (r >= R) return 0u;
+      const uint32_t v = a.wtab[size_t(r * K + j) * kNibWords + e];
+      return high ? (v >> 16) : (v & 0xFFFFu);
+    };
+    reinterpret_cast<uint32_t*>(lds)[i] = word(1 + 2 * pr) | (word(2 + 2 * pr) << 16);
+  }
+  __syncthreads();
+  const kptr* sp = (const kptr*)a.src;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[a.row0 + r];
+  const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(static_cast<void*>(lds)));
+  const int64_t nblk = (a.nvec + kBlock - 1) / kBlock;
+  for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const int64_t col = b * kBlock + threadIdx.x;
+    if (col >= a.nvec) continue;
+    uint32_t lo[4][EW], hi[4][EW];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int q = 0; q < EW; ++q) lo[c][q] = hi[c][q] = 0u;
+    u32x4 x0 = load16t<1>(sp[0], col);  // column 0: into every row
+    u32x4 row0 = x0;                     // row 0: XOR of the sources
+    for (int j0 = 1; j0 < K; j0 += CHUNK) {
+      u32x4 xs[CHUNK];
+#pragma unroll
+      for (int u = 0; u < CHUNK; ++u)
+        if (j0 + u < K) xs[u] = load16t<1>(sp[j0 + u], col);
+#pragma unroll
+      for (int u = 0; u < CHUNK; ++u) {
+        const int j = j0 + u;
+        if (j >= K) break;
+        row0 ^= xs[u];
+        const uint32_t jbase = lds_base + uint32_t(j - 1) * uint32_t(nib16_source_bytes(L));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t x = xs[u][c];
+          constexpr int kSh = EB == 8 ? 3 : 2;
+          constexpr uint32_t kNibMask = 0x0F0F0F0Fu << kSh;
+          const uint32_t ns[2] = {(x << kSh) & kNibMask, (x >> (4 - kSh)) & kNibMask};
+#pragma unroll
+          for (int g = 0; g < GROUPS; ++g) {
+            constexpr int TN = 8 / GROUPS;
+            uint32_t v[TN][EW];
+#pragma unroll
+            for (int tt = 0; tt < TN; ++tt) {
+              const int t = g * TN + tt;
+              const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
+                                  uint32_t(t * 16 * EB);
+              if constexpr (EW == 1) {
+                v[tt][0] = *(lds_u32c*)(size_t(ad));
+              } else {
+                const u32x2 q = *(lds_u32x2c*)(size_t(ad));
+                v[tt][0] = q.x;
+                v[tt][1] = q.y;
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < EW; ++q) {
+#pragma unroll
+              for (int tt = 0; tt < TN; tt += 2) {
+                const int t = g * TN + tt;
+                if (t < 4) lo[c][q] = xor3(lo[c][q], v[tt][q], v[tt + 1][q]);
+                else hi[c][q] = xor3(hi[c][q], v[tt][q], v[tt + 1][q]);
+              }
+            }
+          }
+        }
+      }
+    }
+    store16t<1>(dp[0], col, row0);
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      u32x4 o;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        o[c] = __builtin_amdgcn_perm(hi[c][(r - 1) >> 1], lo[c][(r - 1) >> 1], ((r - 1) & 1) ? 0x07060302u : 0x05040100u) ^
+               x0[c];
+      store16t<1>(dp[r], col, o);
+    }
+  }
+}
+
 template <int R, int U, bool B128>
 constexpr unsigned split_lds(int K) {
   constexpr int L = R - U;
@@ -377,6 +475,15 @@ int main(int argc, char** argv) {
       vs.push_back({"prod_nib16_4_grid" + std::to_string(b), reinterpret_cast<const void*>(&gf_apply_wide_nib16<4>), l16, b});
     for (int b : {2, 3, 4})
       vs.push_back({"n16_c2_g2_grid" + std::to_string(b), reinterpret_cast<const void*>(&lab::nib16v<4, 2, 2>), l16, b});
+    if (unit_rc) {
+      const unsigned lu = unsigned((K - 1) * nib16_source_bytes(3));
+      for (int b : {0, 2, 3, 4}) {
+        const std::string gs = b ? "_grid" + std::to_string(b) : "";
+        vs.push_back({"n16u_c8_g1" + gs, reinterpret_cast<const void*>(&lab::nib16u<4, 8, 1>), lu, b});
+        vs.push_back({"n16u_c4_g2" + gs, reinterpret_cast<const void*>(&lab::nib16u<4, 4, 2>), lu, b});
+        vs.push_back({"n16u_c3_g1" + gs, reinterpret_cast<const void*>(&lab::nib16u<4, 3, 1>), lu, b});
+      }
+    }
   }
   int dev = 0, cus = 0;
   CK(hipGetDevice(&dev));

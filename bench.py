@@ -74,6 +74,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the per-config block (C2 / C3 / C4 / C5 launches, N = 1 only)")
+    ap.add_argument("--e2e-stripes", type=int, default=24,
+                    help="pinned host stripes for the PCIe-inclusive e2e rate on rank 0 (0 = skip)")
     ap.add_argument("--spawn-selftest", action="store_true",
                     help="launch / rendezvous / report path only, no GPU work (CPU test of --gpus N)")
     return ap.parse_args(argv)
@@ -403,6 +405,61 @@ def copy_ceiling(slab, shard, reps: int = 10):
                       f"{'nt' if policy & 2 else 'plain'}), median of {reps}"}
 
 
+def e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes: int = 24, depth: int = 3):
+    """The north star's PCIe-inclusive rate (never `value`): `stripes` stripes
+    of pinned host shards through the host pipelines, i.e. H2D, code and D2H
+    of consecutive stripes overlapped on three HIP streams (client write path
+    client_main.cpp:1714-1815: data in, parity out; read path :2055-2182:
+    survivors in, the erased shards out).  Rank 0 only, after every rank's
+    timed work: the link and the host memory are not shared with the timed
+    region.  Data GiB/s = k * S per stripe over the wall time of one pass
+    (the first pass warms the pipelines); the last stripe's parity is checked
+    against a device-resident encode of the same data, the decode against the
+    shards it rebuilt."""
+    import torch
+    host = torch.empty((stripes, k + m, S), dtype=torch.uint8).pin_memory()
+    g = torch.Generator(device=dev).manual_seed(0xE2E)
+    src = torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g)
+    for s in range(stripes):
+        host[s, :k].copy_(src)
+        host[s, 0, :8].fill_(s)  # stripes differ
+    torch.cuda.synchronize(dev)
+
+    def timed_pass(p):
+        def run():
+            for s in range(stripes):
+                p.submit([host[s, j] for j in range(k)], [host[s, k + i] for i in range(m)])
+            p.drain()
+        run()
+        t0 = time.perf_counter()
+        run()
+        return time.perf_counter() - t0
+
+    out = {"workload": f"RS({k},{m}) {S >> 20} MiB shards, {stripes} stripes of pinned host memory, "
+                       f"pipeline depth {depth}, one GPU's PCIe link",
+           "unit": "GiB/s of data shards", "note": "PCIe-inclusive; not the bench value (inputs resident in HBM)"}
+    enc = E.HostPipeline(k, m, M, S, depth=depth, device=dev.index)
+    t = timed_pass(enc)
+    enc.close()
+    last = host[stripes - 1]
+    d = last[:k].to(dev)
+    ref = torch.empty((m, S), dtype=torch.uint8, device=dev)
+    E.encode_plan(k, m, M, dev.index).bind([[d[j] for j in range(k)]], [[ref[i] for i in range(m)]], S).launch()
+    torch.cuda.synchronize(dev)
+    out["encode"] = {"data_GiBps": round(stripes * k * S / t / 2**30, 2), "pass_ms": round(t * 1e3, 2),
+                     "parity_ok": bool(torch.equal(ref.cpu(), last[k:]))}
+    if erasures:
+        want = last.clone()
+        dec = E.HostPipeline.decoder(k, m, M, erasures, S, depth=depth, device=dev.index)
+        host[:, erasures] = 0  # every stripe's erased shards are rebuilt by the timed passes
+        t = timed_pass(dec)
+        dec.close()
+        out["decode"] = {"erasures": erasures, "data_GiBps": round(stripes * k * S / t / 2**30, 2),
+                         "pass_ms": round(t * 1e3, 2), "rebuilt_ok": bool(torch.equal(host[stripes - 1], want))}
+    del host
+    return out
+
+
 def load_traffic(name: str, workload_key: str, kernel_id: str, profiles_dir: str = ""):
     """(HBM bytes per launch, note) from the committed rocprofv3 PMC summary
     (profiles/pmc_<name>.json, written by profiles/summarize.py from separate
@@ -698,6 +755,9 @@ def main(argv=None):
             if host_has_avx2() and os.path.exists(REFERENCE_O3_SO):
                 cpu_o3, ok_o3 = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_stripe, k, m, erasures, o3=True)
                 cpu_ok = cpu_ok and ok_o3
+        # about 1.5 GiB of pinned host memory at most (C3: 24 stripes, C5: 6)
+        e2e_n = min(args.e2e_stripes, max(2, (3 << 29) // ((k + m) * S)))
+        e2e = e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes=e2e_n) if args.e2e_stripes > 0 else None
         achieved = enc_bytes / (enc_ms / 1e3) / 1e9
         wkey = f"{args.config}:{B}"
         kernel_id = N.lib.ecgpu_build_id(1).decode()
@@ -744,11 +804,14 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "cpu_baseline_o3": cpu_o3,
+            "e2e": e2e,
             "selfcheck_parity_ok": ok,
             "selfcheck_vs_reference_cpu": cpu_ok,
             "build_id": {"library": N.lib.ecgpu_build_id(0).decode(), "kernels": kernel_id},
         }
         print(json.dumps(out), flush=True)
+        if e2e and not (e2e["encode"]["parity_ok"] and e2e.get("decode", {}).get("rebuilt_ok", True)):
+            ok = False
     barrier(world)
     if world > 1:
         import torch.distributed as dist

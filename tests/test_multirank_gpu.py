@@ -172,6 +172,10 @@ def test_bench_gpus2_rehearsal_spawns_two_ranks(gpu):
                 "C4_decode_0123", "C5_encode"} <= set(p["configs"])
         assert p["configs"]["C4_decode_0123"]["frac"] > 0
     assert d["configs"]["C3_decode_parity"]["algorithmic_bytes_per_launch"] == 11 * (4 << 20) * 4
+    # rank 0's PCIe-inclusive host-pipeline rates, after every rank's timed work
+    e2e = d["e2e"]
+    assert e2e["encode"]["parity_ok"] and e2e["encode"]["data_GiBps"] > 1
+    assert e2e["decode"]["rebuilt_ok"] and e2e["decode"]["erasures"] == [0]
 
 
 def test_bench_gpus_beyond_visible_devices_fails(gpu):
@@ -190,3 +194,4 @@ def test_bench_config_c5(gpu):
     assert d["config"]["workload"].startswith("C5: RS(12,4)")
     assert (d["config"]["k"], d["config"]["m"], d["config"]["shard_bytes"]) == (12, 4, 16 << 20)
     assert d["decode_kernel"] is None and d["selfcheck_parity_ok"] is True
+    assert d["e2e"]["encode"]["parity_ok"] and "decode" not in d["e2e"]  # C5 has no decode

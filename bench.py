@@ -405,6 +405,62 @@ def copy_ceiling(slab, shard, reps: int = 10):
                       f"{'nt' if policy & 2 else 'plain'}), median of {reps}"}
 
 
+def mix_ceiling(slab, shard, k, m, reps: int = 10):
+    """The ceiling of the encode's own access mix: the diagnostic kernel
+    diag_xor_mix<k, m> (libecgpu_diag.so variant 16) issues exactly the
+    coding launch's streams -- k non-temporal 16-B loads and m non-temporal
+    16-B stores per lane over the same slab, shard stride and grid -- with one
+    XOR instead of the GF(2^8) multiplies.  GB/s of (k + m) * S per stripe,
+    best of uncapped and 3 / 4 resident workgroups per CU (the production
+    residency caps, an unused dynamic LDS allocation); None without the
+    library or for a (k, m) it does not instantiate."""
+    import ctypes
+
+    import torch
+
+    from erasure_coding_test_amd import _native as N
+    path = os.path.join(N.LIB_DIR, "libecgpu_diag.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    L.ecgpu_diag_launch.restype = ctypes.c_int
+    L.ecgpu_diag_launch.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p] * 4 + [
+        ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_void_p,
+        ctypes.c_void_p]
+    B = slab.shape[0]
+    dev = slab.device
+    src = torch.tensor([slab[b, j].data_ptr() for b in range(B) for j in range(k)], dtype=torch.int64, device=dev)
+    dst = torch.tensor([slab[b, k + i].data_ptr() for b in range(B) for i in range(m)], dtype=torch.int64,
+                       device=dev)
+    stream = torch.cuda.current_stream(dev)
+    lds_per_cu = 160 << 10  # MI355X (gfx950) LDS per CU
+    best = None
+    saved = os.environ.get("ECGPU_DIAG_LDS")
+    try:
+        for blocks in (0, 3, 4):
+            os.environ["ECGPU_DIAG_LDS"] = str((lds_per_cu // blocks) & ~511 if blocks else 0)
+            rc = [0]
+
+            def go():
+                rc[0] = rc[0] or L.ecgpu_diag_launch(16, k, m, 1, 0, None, None, src.data_ptr(), dst.data_ptr(),
+                                                     B, shard, 0, 0, 1, stream.cuda_stream, None)
+            ms = time_launches(go, stream, reps, warmup=2)
+            if rc[0] != 0:
+                return None
+            if best is None or ms < best[0]:
+                best = (ms, blocks)
+    finally:
+        if saved is None:
+            os.environ.pop("ECGPU_DIAG_LDS", None)
+        else:
+            os.environ["ECGPU_DIAG_LDS"] = saved
+    ms, blocks = best
+    return {"GBps": round((k + m) * shard * B / (ms / 1e3) / 1e9, 1), "median_launch_ms": round(ms, 4),
+            "kernel": f"diag_xor_mix<{k},{m}>: the encode's {k} nt loads + {m} nt stores of 16 B per lane, one "
+                      f"XOR, no multiplies; {'uncapped' if not blocks else f'{blocks} workgroups per CU'} "
+                      f"(best of uncapped / 3 / 4), median of {reps}"}
+
+
 def e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes: int = 24, depth: int = 3):
     """The north star's PCIe-inclusive rate (never `value`): `stripes` stripes
     of pinned host shards through the host pipelines, i.e. H2D, code and D2H
@@ -720,6 +776,7 @@ def main(argv=None):
         main_entries.update(c3_decode_shapes(E, shards, S, B, dev, stream, kind, bool(args.nt)))
     del enc, dec, ref
     copy = copy_ceiling(slab, S)  # after the parity checks: the copy overwrites the slab's second half
+    mix = mix_ceiling(slab, S, k, m)  # overwrites the parity shards
     configs = None
     if not args.no_configs:
         del shards
@@ -734,7 +791,8 @@ def main(argv=None):
             "decode_frac": (round(dec_bytes / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if dec_ms is not None
                             else None),
             "stripe_ids": [ids[0], ids[-1], len(ids)], "parity_ok": ok,
-            "copy_ceiling_GBps": copy["GBps"] if copy else None}
+            "copy_ceiling_GBps": copy["GBps"] if copy else None,
+            "mix_ceiling_GBps": mix["GBps"] if mix else None}
     if configs:
         mine["configs"] = {name: {"median_launch_ms": e["median_launch_ms"], "frac": e["frac"]}
                            for name, e in configs.items()}
@@ -792,6 +850,8 @@ def main(argv=None):
                          "read_only_frac": round(k * S * B / (enc_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
             "copy_ceiling": copy,
             "encode_frac_of_copy": round(achieved / copy["GBps"], 4) if copy else None,
+            "mix_ceiling": mix,
+            "encode_frac_of_mix": round(achieved / mix["GBps"], 4) if mix else None,
             "decode_kernel": ({"erasures": erasures, "median_launch_ms": round(dec_ms, 4),
                                "algorithmic_bytes_per_launch": dec_bytes,
                                "achieved_GBps": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),

@@ -13,6 +13,10 @@
 //              explicit sc0 / sc1 / nt cache bits (cache-policy probe)
 //   variant 10: production gf_apply with the round-1 2-bit-slice tables
 //              (A/B against variants 4/8, which use the 3-bit-slice ptab)
+//   variant 16: diag_xor_mix<K, R> -- the coding launches' exact streams (K
+//              nt loads and R nt stores of 16 B per lane, one column per
+//              lane, production grid) with no arithmetic beyond one XOR: the
+//              ceiling of a K-read / R-write mix (bench.py `mix_ceiling`)
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -32,6 +36,28 @@ namespace {
 __device__ __forceinline__ void sink(const ApplyArgs& a, int s, int64_t col, const u32x4& acc) {
   if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u && acc.z == 0x85EBCA6Bu && acc.w == 0xC2B2AE35u)
     ecgpu::dev::store16(a.dst[int64_t(s) * a.dst_stride], col, acc, 1);
+}
+
+// ---- access-mix ceiling (variant 16): every lane loads its 16-B column of
+// the K sources (non-temporal, all issued before use, like gf_apply), folds
+// them with XOR and stores the result to the R outputs (non-temporal).
+template <int K, int R>
+__global__ __launch_bounds__(256) void diag_xor_mix(ApplyArgs a) {
+  const int64_t col = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* dp[R];  // every pointer before the first store
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + r];
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = ecgpu::dev::load16t<1>(sp[j], col);
+  u32x4 acc = x[0];
+#pragma unroll
+  for (int j = 1; j < K; ++j) acc ^= x[j];
+#pragma unroll
+  for (int r = 0; r < R; ++r) ecgpu::dev::store16t<1>(dp[r], col, acc);
 }
 
 // ---- cache-policy probe (variant 15): the production combine with loads
@@ -263,6 +289,12 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
     vec = 1;
     if (K == 10 && R == 4) fn = pick_pol<10, 4, 3>(lp, mode);
     if (K == 10 && R == 1) fn = pick_pol<10, 1, 4>(lp, mode);
+  } else if (variant == 16) {
+    vec = 1;
+    if (K == 10 && R == 4) fn = &diag_xor_mix<10, 4>;
+    if (K == 10 && R == 1) fn = &diag_xor_mix<10, 1>;
+    if (K == 6 && R == 3) fn = &diag_xor_mix<6, 3>;
+    if (K == 12 && R == 4) fn = &diag_xor_mix<12, 4>;
   } else if (variant == 2) {
     vec = 1;
     if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_lds<10, 4>;

@@ -405,15 +405,17 @@ def copy_ceiling(slab, shard, reps: int = 10):
                       f"{'nt' if policy & 2 else 'plain'}), median of {reps}"}
 
 
-def mix_ceiling(slab, shard, k, m, reps: int = 10):
-    """The ceiling of the encode's own access mix: the diagnostic kernel
-    diag_xor_mix<k, m> (libecgpu_diag.so variant 16) issues exactly the
-    coding launch's streams -- k non-temporal 16-B loads and m non-temporal
-    16-B stores per lane over the same slab, shard stride and grid -- with one
-    XOR instead of the GF(2^8) multiplies.  GB/s of (k + m) * S per stripe,
-    best of uncapped and 3 / 4 resident workgroups per CU (the production
-    residency caps, an unused dynamic LDS allocation); None without the
-    library or for a (k, m) it does not instantiate."""
+def xor_stream_probe(slab, shard, k, m, reps: int = 10):
+    """The coding launch's own streams without its arithmetic: the
+    diagnostic kernel diag_xor_mix<k, m> (libecgpu_diag.so variant 16) issues
+    k non-temporal 16-B loads and m non-temporal 16-B stores per lane over
+    the same slab, shard stride and grid, with one XOR instead of the GF(2^8)
+    multiplies.  A reference point for "is the arithmetic in the way?", NOT an
+    upper bound: the arithmetic also spaces the stores out, and the real
+    encode beats the probe on some shapes.  GB/s of (k + m) * S
+    per stripe, best of uncapped and 3 / 4 resident workgroups per CU (the
+    production residency caps, an unused dynamic LDS allocation); None
+    without the library or for a (k, m) it does not instantiate."""
     import ctypes
 
     import torch
@@ -459,6 +461,14 @@ def mix_ceiling(slab, shard, k, m, reps: int = 10):
             "kernel": f"diag_xor_mix<{k},{m}>: the encode's {k} nt loads + {m} nt stores of 16 B per lane, one "
                       f"XOR, no multiplies; {'uncapped' if not blocks else f'{blocks} workgroups per CU'} "
                       f"(best of uncapped / 3 / 4), median of {reps}"}
+
+
+def with_mix(entry, mix):
+    """A configs entry against the XOR probe of its own streams (xor_stream_probe)."""
+    if entry is not None and mix:
+        entry["xor_probe_GBps"] = mix["GBps"]
+        entry["vs_xor_probe"] = round(entry["achieved_GBps"] / mix["GBps"], 4)
+    return entry
 
 
 def e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes: int = 24, depth: int = 3):
@@ -593,8 +603,8 @@ def config_block(E, N, dev, stream, kind, nt, main=None):
         ms = time_launches(lambda: p.launch(stream.cuda_stream), stream, CFG_REPS, warmup=CFG_WARMUP)
         e = {"workload": f"RS({k},{m}) encode, {S >> 20} MiB shards, {B} stripes"}
         e.update(roofline_entry((k + m) * S * B, ms))
-        out[name] = e
         p.close()
+        out[name] = with_mix(e, xor_stream_probe(slab, S, k, m))  # after the timing: overwrites the parity
         del slab, shards
 
     encode_cfg("C2_encode", 6, 3, 1 << 20, 512, 2)
@@ -635,8 +645,8 @@ def config_block(E, N, dev, stream, kind, nt, main=None):
     e["host_note"] = ("host_decode_plan_us: ecgpu_decode_plan (survivor choice, k x k inversion, fused map) through "
                       "ctypes; host_plan_create_us: the whole DecodePlan incl. coefficient tables and their (asynchronous) upload; "
                       "medians, not in the launch time")
-    out["C4_decode_0123"] = e
     dp.close()
+    out["C4_decode_0123"] = with_mix(e, xor_stream_probe(slab, S, k, m))  # the same 10-read / 4-write streams
     del slab, shards
     encode_cfg("C5_encode", 12, 4, 16 << 20, 24, 5)
     torch.cuda.synchronize(dev)
@@ -776,7 +786,12 @@ def main(argv=None):
         main_entries.update(c3_decode_shapes(E, shards, S, B, dev, stream, kind, bool(args.nt)))
     del enc, dec, ref
     copy = copy_ceiling(slab, S)  # after the parity checks: the copy overwrites the slab's second half
-    mix = mix_ceiling(slab, S, k, m)  # overwrites the parity shards
+    mix = xor_stream_probe(slab, S, k, m)  # overwrites the parity shards
+    if main_entries:
+        with_mix(main_entries["C3_encode"], mix)
+        mix_dec = xor_stream_probe(slab, S, k, 1)  # every C3 decode shape reads 10 shards and writes 1
+        for name in ("C3_decode_0", "C3_decode_data_random", "C3_decode_parity"):
+            with_mix(main_entries.get(name), mix_dec)
     configs = None
     if not args.no_configs:
         del shards
@@ -792,7 +807,7 @@ def main(argv=None):
                             else None),
             "stripe_ids": [ids[0], ids[-1], len(ids)], "parity_ok": ok,
             "copy_ceiling_GBps": copy["GBps"] if copy else None,
-            "mix_ceiling_GBps": mix["GBps"] if mix else None}
+            "xor_probe_GBps": mix["GBps"] if mix else None}
     if configs:
         mine["configs"] = {name: {"median_launch_ms": e["median_launch_ms"], "frac": e["frac"]}
                            for name, e in configs.items()}
@@ -850,8 +865,8 @@ def main(argv=None):
                          "read_only_frac": round(k * S * B / (enc_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
             "copy_ceiling": copy,
             "encode_frac_of_copy": round(achieved / copy["GBps"], 4) if copy else None,
-            "mix_ceiling": mix,
-            "encode_frac_of_mix": round(achieved / mix["GBps"], 4) if mix else None,
+            "xor_stream_probe": mix,
+            "encode_vs_xor_probe": round(achieved / mix["GBps"], 4) if mix else None,
             "decode_kernel": ({"erasures": erasures, "median_launch_ms": round(dec_ms, 4),
                                "algorithmic_bytes_per_launch": dec_bytes,
                                "achieved_GBps": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),

@@ -15,8 +15,9 @@
 //              (A/B against variants 4/8, which use the 3-bit-slice ptab)
 //   variant 16: diag_xor_mix<K, R> -- the coding launches' exact streams (K
 //              nt loads and R nt stores of 16 B per lane, one column per
-//              lane, production grid) with no arithmetic beyond one XOR: the
-//              ceiling of a K-read / R-write mix (bench.py `mix_ceiling`)
+//              lane, production grid) with no arithmetic beyond one XOR: a
+//              reference point for the coding kernels' streams, not a bound
+//              (bench.py `xor_stream_probe`)
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>

@@ -33,18 +33,23 @@ ECGPU_API void ecgpu_free(void* p) { std::free(p); }
 // per launch, every skew's slab interleaved, tools/skew_sweep.sh) gave the same
 // numbers within ~1 % on three MI355X boxes (profiles/r03_skew_sweep_*.jsonl),
 // including sharp dips of 15-30 % (e.g. +12 KiB at 1 and 3 MiB shards, +8 KiB
-// at 2 and 6 MiB, +14 KiB at 512 KiB, no skew from 4 MiB up).  For the shard
-// sizes measured, the skew with the best worst-box rate; tie-breaks from the
-// BASELINE configs' own in-process A/Bs (RS(6,3) 1 MiB: none, 2-3 % over
-// +10 KiB; RS(10,4) 4 MiB: +14 KiB, 1.5-2 %; RS(12,4) 16 MiB: +8 KiB, 4-5 %;
-// profiles/r03_skew_ab.jsonl).  Other sizes keep +10 KiB, which is within
-// 1-4 % of the best at every size measured and never near a dip.
+// at 2 and 6 MiB, +14 KiB at 512 KiB, no skew from 4 MiB up), and again on
+// independent random shards (profiles/r03_skew_sweep_random.jsonl; the first
+// sweeps filled every shard from one buffer, and HBM throughput depends on the
+// data).  For the shard sizes measured, the skew with the best
+// rate; tie-breaks from the BASELINE configs' own A/Bs on random data:
+// RS(6,3) 1 MiB none (1-3 % over +10 KiB, profiles/r03_skew_ab_random.jsonl);
+// RS(10,4) 4 MiB +6 KiB, the best bench step (encode + decode{0}) on three
+// boxes, 0.6-1 % over the +14 KiB first chosen on the old fill
+// (profiles/r03_skew_step_ab.jsonl); RS(12,4) 16 MiB +8 KiB (4 %).  Other
+// sizes keep +10 KiB, within 1-4 % of the best at every size measured and
+// never near a dip.
 struct SkewClass {
   int64_t size, skew;
 };
 constexpr SkewClass kSkewTable[] = {
     {256 << 10, 12 << 10}, {512 << 10, 8 << 10},  {1 << 20, 0},          {2 << 20, 12 << 10},
-    {3 << 20, 8 << 10},    {4 << 20, 14 << 10},   {6 << 20, 12 << 10},   {8 << 20, 12 << 10},
+    {3 << 20, 8 << 10},    {4 << 20, 6 << 10},   {6 << 20, 12 << 10},   {8 << 20, 12 << 10},
     {12 << 20, 8 << 10},   {16 << 20, 8 << 10},   {32 << 20, 8 << 10},   {64 << 20, 8 << 10},
 };
 constexpr int64_t kDefaultSkew = 10 << 10;

@@ -181,8 +181,8 @@ def test_recommended_stride():
     from erasure_coding_test_amd import _native as N
     # per-size skew table (capi_host.cpp kSkewTable, profiles/r03_skew_sweep_*.jsonl), +10 KiB elsewhere
     st = N.lib.ecgpu_recommended_shard_stride
-    assert st(4 << 20) == (4 << 20) + (14 << 10)
-    assert st((4 << 20) + 3) == (4 << 20) + 256 + (14 << 10)
+    assert st(4 << 20) == (4 << 20) + (6 << 10)
+    assert st((4 << 20) + 3) == (4 << 20) + 256 + (6 << 10)
     assert st(16 << 20) == (16 << 20) + (8 << 10)
     assert st(1 << 20) == 1 << 20
     assert st(5 << 20) == (5 << 20) + (10 << 10)

@@ -191,6 +191,22 @@ def test_recommended_stride():
         assert st(size) % 256 == 0 and st(size) >= size
 
 
+def test_stride_skew_override(monkeypatch):
+    """ECGPU_SHARD_SKEW_KIB replaces the per-size table (read per call);
+    malformed or out-of-range values are ignored."""
+    from erasure_coding_test_amd import _native as N
+    st = N.lib.ecgpu_recommended_shard_stride
+    monkeypatch.setenv("ECGPU_SHARD_SKEW_KIB", "12")
+    assert st(4 << 20) == (4 << 20) + (12 << 10) and st(1 << 20) == (1 << 20) + (12 << 10)
+    monkeypatch.setenv("ECGPU_SHARD_SKEW_KIB", "0")
+    assert st(16 << 20) == 16 << 20
+    for bad in ("", "x", "12k", "-4", "2000"):
+        monkeypatch.setenv("ECGPU_SHARD_SKEW_KIB", bad)
+        assert st(4 << 20) == (4 << 20) + (6 << 10), bad
+    monkeypatch.delenv("ECGPU_SHARD_SKEW_KIB")
+    assert st(4 << 20) == (4 << 20) + (6 << 10)
+
+
 NO_GPU = not os.path.exists("/dev/kfd")
 
 

@@ -55,7 +55,34 @@ __global__ __launch_bounds__(BS) void enc_bs(ApplyArgs a) {
   for (int j = 0; j < K; ++j) x[j] = load16t<1>(sp[j], col);
   combine_store<K, R, UNITS, 3, 1>(a, x, dp, col);
 }
+
+// Early unit row: for a Vandermonde encode (row 0 and column 0 all ones) row
+// 0 is the XOR of the sources, stored right after the loads, before the
+// multiply rows 1..R-1 are computed (production stores all R rows at the end).
+template <int K, int R>
+__global__ __launch_bounds__(256) void enc_early0(ApplyArgs a) {
+  const int64_t col = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = load16t<1>(sp[j], col);
+  u32x4 r0 = x[0];
+#pragma unroll
+  for (int j = 1; j < K; ++j) r0 ^= x[j];
+  store16t<1>(dp[0], col, r0);
+  u32x4 acc[R - 1];
+  combine3<K, R - 1, kUnitCol0>((const kconst_u32*)a.ptab + K * kP3Words, x, acc);  // rows 1..R-1
+#pragma unroll
+  for (int r = 1; r < R; ++r) store16t<1>(dp[r], col, acc[r - 1]);
+}
 }  // namespace lab
+
+bool g_early0 = false;  // --early0 1: skew mode also times lab::enc_early0 on every slab
 
 struct Variant {
   std::string name;
@@ -109,6 +136,7 @@ int main(int argc, char** argv) {
     else if (f == "--m") mm = std::atoi(argv[i + 1]);
     else if (f == "--mib") kib = 1024 * std::atoi(argv[i + 1]);
     else if (f == "--kib") kib = std::atoi(argv[i + 1]);
+    else if (f == "--early0") g_early0 = std::atoi(argv[i + 1]) != 0;
     else if (f == "--skews") {
       std::string v = argv[i + 1];
       size_t p = 0;
@@ -291,12 +319,13 @@ int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int
   const unsigned lds = unsigned(lds_cu / blocks) & ~511u;
   constexpr int U = kUnitCol0 | kUnitRow0;
   const void* fn = reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>);
+  const void* fn_e = reinterpret_cast<const void*>(&lab::enc_early0<k, m>);
   struct Slab {
     int skew;
     uint8_t* base;
     size_t stride;
     ApplyArgs a;
-    std::vector<float> t;
+    std::vector<float> t, te;
   };
   std::vector<Slab> slabs;
   const std::vector<uint8_t> h = random_pool(S, 17);
@@ -335,13 +364,16 @@ int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int
     a.nt = 1;
     slabs.push_back(sl);
   }
-  auto launch = [&](Slab& sl) {
+  auto launch = [&](Slab& sl, const void* f = nullptr) {
     ApplyArgs args = sl.a;
     void* kargs[] = {&args};
-    CK(hipLaunchKernel(fn, dim3(unsigned((sl.a.nvec + 255) / 256), unsigned(stripes)), dim3(256), kargs, lds, nullptr));
+    CK(hipLaunchKernel(f ? f : fn, dim3(unsigned((sl.a.nvec + 255) / 256), unsigned(stripes)), dim3(256), kargs, lds,
+                       nullptr));
   };
-  for (auto& sl : slabs) {  // host spot check of stripe 0 and the last
-    launch(sl);
+  for (int pass = 0; pass < (g_early0 ? 2 : 1); ++pass)
+  for (auto& sl : slabs) {  // host spot check of stripe 0 and the last (pass 1: enc_early0)
+    if (pass == 1) CK(hipMemset(sl.base + sl.stride * size_t(k), 0, sl.stride * size_t(m)));  // stripe 0's parity
+    launch(sl, pass ? fn_e : fn);
     CK(hipDeviceSynchronize());
     std::mt19937_64 q(9);
     for (int n = 0; n < 64; ++n) {
@@ -376,6 +408,17 @@ int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int
         CK(hipEventElapsedTime(&ms, e0, e1));
         sl.t.push_back(ms * 1000.f);
       }
+      if (!g_early0) continue;
+      for (int w = 0; w < 2; ++w) launch(sl, fn_e);
+      for (int q = 0; q < reps; ++q) {
+        CK(hipEventRecord(e0, nullptr));
+        launch(sl, fn_e);
+        CK(hipEventRecord(e1, nullptr));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        sl.te.push_back(ms * 1000.f);
+      }
     }
   const double bytes = double(k + m) * double(S) * stripes;
   for (auto& sl : slabs) {
@@ -384,6 +427,12 @@ int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int
     std::printf("{\"k\": %d, \"m\": %d, \"shard_kib\": %d, \"stripes\": %d, \"skew_kib\": %d, \"median_us\": %.1f, "
                 "\"min_us\": %.1f, \"GBps\": %.0f, \"frac\": %.4f}\n",
                 k, m, kib, stripes, sl.skew, med, double(sl.t[0]), bytes / med / 1e3, bytes / med / 1e3 / 8000.0);
+    if (!g_early0) continue;
+    std::sort(sl.te.begin(), sl.te.end());
+    const double me = sl.te[sl.te.size() / 2];
+    std::printf("{\"variant\": \"early0\", \"k\": %d, \"m\": %d, \"shard_kib\": %d, \"stripes\": %d, \"skew_kib\": %d, "
+                "\"median_us\": %.1f, \"min_us\": %.1f, \"GBps\": %.0f, \"vs_prod\": %.4f}\n",
+                k, m, kib, stripes, sl.skew, me, double(sl.te[0]), bytes / me / 1e3, med / me);
   }
   return 0;
 }

@@ -83,6 +83,7 @@ __global__ __launch_bounds__(256) void enc_early0(ApplyArgs a) {
 }  // namespace lab
 
 bool g_early0 = false;  // --early0 1: skew mode also times lab::enc_early0 on every slab
+bool g_vec2 = false;    // --vec2 1: ... and the production body with two columns per lane (VEC = 2)
 
 struct Variant {
   std::string name;
@@ -137,6 +138,7 @@ int main(int argc, char** argv) {
     else if (f == "--mib") kib = 1024 * std::atoi(argv[i + 1]);
     else if (f == "--kib") kib = std::atoi(argv[i + 1]);
     else if (f == "--early0") g_early0 = std::atoi(argv[i + 1]) != 0;
+    else if (f == "--vec2") g_vec2 = std::atoi(argv[i + 1]) != 0;
     else if (f == "--skews") {
       std::string v = argv[i + 1];
       size_t p = 0;
@@ -319,7 +321,10 @@ int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int
   const unsigned lds = unsigned(lds_cu / blocks) & ~511u;
   constexpr int U = kUnitCol0 | kUnitRow0;
   const void* fn = reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>);
-  const void* fn_e = reinterpret_cast<const void*>(&lab::enc_early0<k, m>);
+  const void* fn_e = g_vec2 ? reinterpret_cast<const void*>(&gf_apply<k, m, U, 2, 3, 3>)
+                            : reinterpret_cast<const void*>(&lab::enc_early0<k, m>);
+  const int per_e = g_vec2 ? 512 : 256;  // columns per workgroup of the variant
+  if (g_vec2) g_early0 = true;           // the variant slot times VEC = 2 instead
   struct Slab {
     int skew;
     uint8_t* base;
@@ -367,8 +372,9 @@ int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int
   auto launch = [&](Slab& sl, const void* f = nullptr) {
     ApplyArgs args = sl.a;
     void* kargs[] = {&args};
-    CK(hipLaunchKernel(f ? f : fn, dim3(unsigned((sl.a.nvec + 255) / 256), unsigned(stripes)), dim3(256), kargs, lds,
-                       nullptr));
+    const int per = f == fn_e ? per_e : 256;
+    CK(hipLaunchKernel(f ? f : fn, dim3(unsigned((sl.a.nvec + per - 1) / per), unsigned(stripes)), dim3(256), kargs,
+                       lds, nullptr));
   };
   for (int pass = 0; pass < (g_early0 ? 2 : 1); ++pass)
   for (auto& sl : slabs) {  // host spot check of stripe 0 and the last (pass 1: enc_early0)
@@ -430,9 +436,9 @@ int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int
     if (!g_early0) continue;
     std::sort(sl.te.begin(), sl.te.end());
     const double me = sl.te[sl.te.size() / 2];
-    std::printf("{\"variant\": \"early0\", \"k\": %d, \"m\": %d, \"shard_kib\": %d, \"stripes\": %d, \"skew_kib\": %d, "
+    std::printf("{\"variant\": \"%s\", \"k\": %d, \"m\": %d, \"shard_kib\": %d, \"stripes\": %d, \"skew_kib\": %d, "
                 "\"median_us\": %.1f, \"min_us\": %.1f, \"GBps\": %.0f, \"vs_prod\": %.4f}\n",
-                k, m, kib, stripes, sl.skew, me, double(sl.te[0]), bytes / me / 1e3, med / me);
+                g_vec2 ? "vec2" : "early0", k, m, kib, stripes, sl.skew, me, double(sl.te[0]), bytes / me / 1e3, med / me);
   }
   return 0;
 }

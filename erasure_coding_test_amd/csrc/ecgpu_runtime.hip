@@ -467,6 +467,20 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
         default: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 4> : &dev::gf_apply_wide<4, 4>; break;
       }
     }
+    // The pipelined form of the same kernels (gf_apply_wide_pipe: compile-time
+    // K, the next chunk's loads in flight during this chunk's lookups) for
+    // launches of whole 256-column blocks, where it measured faster: the
+    // w = 32 unit form with K = 7..10 sources (RS(K,4) 64 MiB, in one process:
+    // K = 7 148 -> 139 us, 8 162 -> 149, 10 197 -> 191; K = 5, 11, 12 equal or
+    // slower, and so were the general w = 32 and the w = 16 forms outside
+    // K = 10 -- profiles/r03_wide_lab.jsonl, "r03 pipe K sweep").
+    // ECGPU_WIDE_PIPE: 1 that rule (default), 0 never, 2 every whole-block
+    // launch of every mode (tests, A/B).
+    const int pipe = env_int("ECGPU_WIDE_PIPE", 1);
+    const bool pipe_shape = pipe == 2 || (pipe == 1 && !pack16 && unit_rc && K >= 7 && K <= 10);
+    if (nib && nvec > 0 && nvec % dev::kBlock == 0 && pipe_shape)
+      if (KernelFn f = wide_pipe_kernel(K, R, pack16 ? dev::kPipeW16 : unit_rc ? dev::kPipeW32Unit : dev::kPipeW32))
+        vec_fn = f;
     for (int s0 = 0; s0 < p->stripes; s0 += kMaxGridY) {
       const int ns = std::min(kMaxGridY, p->stripes - s0);
       ApplyArgs a{};

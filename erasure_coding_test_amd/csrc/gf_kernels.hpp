@@ -1403,5 +1403,175 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
   }
 }
 
+// ------------------------------------- wide words, pipelined loads ----
+// The two nibble kernels above with compile-time K and software-pipelined
+// shard loads (production for launches of whole 256-column blocks).  The K
+// sources of a column are NCH (even) chunks of CH, and the chunk sequence is
+// double-buffered across the workgroup's column blocks: chunk c + 1's loads
+// (after the last chunk, the next block's chunk 0) are issued before chunk
+// c's lookups.  Every load and store is unconditional -- the last prefetch
+// re-reads the workgroup's own block and the launch covers whole column
+// blocks -- so the compiler's wait counts are static and a wave waits only
+// for the chunk it is about to look up.  The runtime-K kernels load a chunk
+// and wait for it before any lookup, leaving the wait to other waves to
+// hide (a first pipelined form with conditional loads got vmcnt(0) before
+// every chunk and ran slower).  RS(10,4) 64 MiB, tools/wide_lab.hip in one
+// process: w = 32 195 -> 184-187 us, w = 16 175 -> 170 us
+// (profiles/r03_wide_lab.jsonl, run "r03 pipe static").
+enum WidePipeMode : int { kPipeW32 = 0, kPipeW32Unit = 1, kPipeW16 = 2 };
+
+template <int K, int MODE>
+struct WidePipeShape {
+  // chunks per column: w = 32 four for K = 7..12 (RS(10,4): 3 + 3 + 3 + 1,
+  // 101 VGPRs, 4 workgroups per CU), w = 16 two (5 + 5)
+  static constexpr int NCH = MODE == kPipeW16 ? 2 : 2 * ((K + 5) / 6);
+  static constexpr int CH = (K + NCH - 1) / NCH;
+};
+
+template <int K, int R, int MODE, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_apply_wide_pipe(ApplyArgs a) {
+  constexpr bool W16 = MODE == kPipeW16;
+  constexpr int U = MODE == kPipeW32Unit ? 1 : 0;
+  static_assert(U == 0 || R >= 2, "the unit form needs a row besides the unit row");
+  constexpr int L = R - U;  // rows looked up (w = 32)
+  constexpr int EW = W16 ? nib16_entry_words(R) : nib_entry_words(L), EB = 4 * EW;
+  constexpr uint32_t kSrcBytes = uint32_t(W16 ? nib16_source_bytes(R) : nib_source_bytes(L));
+  constexpr int NCH = WidePipeShape<K, MODE>::NCH, CH = WidePipeShape<K, MODE>::CH;
+  static_assert(NCH % 2 == 0, "buffer parity repeats per column");
+  extern __shared__ __attribute__((aligned(16))) uint8_t nib_lds[];
+  {
+    // the LDS images of gf_apply_wide_nib<R, U> / gf_apply_wide_nib16<R>
+    const int n = (K - U) * kNibWords * EW;
+    for (int i = threadIdx.x; i < n; i += kBlock) {
+      const int l = i % EW, e = (i / EW) % kNibWords, j = i / (EW * kNibWords) + U;
+      uint32_t v;
+      if constexpr (W16) {
+        const bool high = (e >> 4) >= 4;
+        auto word = [&](int r) -> uint32_t {
+          if (r >= R) return 0u;
+          const uint32_t t = a.wtab[size_t(r * K + j) * kNibWords + e];
+          return high ? (t >> 16) : (t & 0xFFFFu);
+        };
+        v = word(2 * l) | (word(2 * l + 1) << 16);
+      } else {
+        v = l < L ? a.wtab[size_t((l + U) * K + j) * kNibWords + e] : 0u;
+      }
+      reinterpret_cast<uint32_t*>(nib_lds)[i] = v;
+    }
+  }
+  __syncthreads();
+
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(static_cast<void*>(nib_lds)));
+  const int64_t nblk = a.nvec / kBlock;  // whole column blocks (host-checked)
+  const int64_t g = gridDim.x;
+  int64_t b = blockIdx.x;
+  if (b >= nblk) return;
+
+  auto load = [&](u32x4 (&x)[CH], int64_t bb, int c) {
+    const int64_t col = bb * kBlock + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      if (c * CH + u < K) x[u] = load16t<1>(kload(sp, c * CH + u), col);  // compile-time test
+  };
+  u32x4 acc[R];            // w = 32: rows
+  uint32_t lo[4][EW], hi[4][EW];  // w = 16: [dword][row pair], low / high word tables
+  auto apply = [&](const u32x4 (&x)[CH], int c) {
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int j = c * CH + u;
+      if (j >= K) break;
+      if (U == 1) {
+        if (j == 0) {  // column 0: a unit in every row
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r] ^= x[u];
+          continue;
+        }
+        acc[0] ^= x[u];  // row 0: units
+      }
+      const uint32_t jbase = lds_base + uint32_t(j - U) * kSrcBytes;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        // nibble t of x scaled by EB in byte t/2 of ns[t & 1] (see gf_apply_wide_nib)
+        constexpr int kSh = EB == 16 ? 4 : EB == 8 ? 3 : 2;
+        constexpr uint32_t kNibMask = 0x0F0F0F0Fu << kSh;
+        const uint32_t xv = x[u][cc];
+        const uint32_t ns[2] = {(xv << kSh) & kNibMask, (xv >> (4 - kSh)) & kNibMask};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // lookups in two groups of four, each folded before the next
+          uint32_t v[4][EW];
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) {
+            const int t = h * 4 + tt;
+            const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
+                                uint32_t(t * 16 * EB);
+            if constexpr (EW == 1) {
+              v[tt][0] = *(lds_u32*)(size_t(ad));
+            } else if constexpr (EW == 2) {
+              const u32x2 q = *(lds_u32x2*)(size_t(ad));
+              v[tt][0] = q.x;
+              v[tt][1] = q.y;
+            } else {
+              const u32x4 q = *(lds_u32x4*)(size_t(ad));
+#pragma unroll
+              for (int l = 0; l < 4; ++l) v[tt][l] = q[l];
+            }
+          }
+          if constexpr (W16) {
+#pragma unroll
+            for (int q = 0; q < EW; ++q) {
+              uint32_t& e = h == 0 ? lo[cc][q] : hi[cc][q];  // tables 0-3 low word, 4-7 high word
+              e = xor3(xor3(e, v[0][q], v[1][q]), v[2][q], v[3][q]);
+            }
+          } else {
+#pragma unroll
+            for (int l = 0; l < L; ++l)
+              acc[l + U][cc] = xor3(xor3(acc[l + U][cc], v[0][l], v[1][l]), v[2][l], v[3][l]);
+          }
+        }
+      }
+    }
+  };
+
+  u32x4 buf[2][CH];
+  load(buf[0], b, 0);
+  for (;;) {
+    const int64_t bn = b + g < nblk ? b + g : b;  // the last prefetch re-reads this block
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+      for (int q = 0; q < EW; ++q) lo[cc][q] = hi[cc][q] = 0u;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c + 1 < NCH)
+        load(buf[(c + 1) & 1], b, c + 1);
+      else
+        load(buf[0], bn, 0);
+      apply(buf[c & 1], c);
+    }
+    const int64_t col = b * kBlock + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (W16) {
+        u32x4 o;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+          o[cc] = __builtin_amdgcn_perm(hi[cc][r >> 1], lo[cc][r >> 1], (r & 1) ? 0x07060302u : 0x05040100u);
+        store16t<1>(dp[r], col, o);
+      } else {
+        store16t<1>(dp[r], col, acc[r]);
+      }
+    }
+    if (bn == b) break;
+    b = bn;
+  }
+}
+
 }  // namespace dev
 }  // namespace ecgpu

@@ -1003,6 +1003,63 @@ def test_wide_word_unit_structured_launches(ec, gpu, monkeypatch, w, nib16, unit
         assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
 
 
+_PIPE_SHAPES = [(1, 1), (2, 2), (3, 4), (5, 3), (6, 4), (7, 2), (10, 4), (12, 4), (13, 3), (16, 4), (10, 6)]
+
+
+@pytest.mark.parametrize("w", [16, 32])
+@pytest.mark.parametrize("structure", ["vandermonde", "random"])
+@pytest.mark.parametrize("k,m", _PIPE_SHAPES)
+@pytest.mark.parametrize("blocks", [3, 1600])
+@pytest.mark.parametrize("pipe", ["2", "1"])
+def test_wide_word_pipelined_launches(ec, gpu, monkeypatch, w, structure, k, m, blocks, pipe):
+    """Launches of whole 256-column blocks (4 KiB per shard each) run
+    gf_apply_wide_pipe<K, R, mode> -- compile-time K, double-buffered source
+    chunks, all three modes (w = 32 unit structure, w = 32 general, w = 16
+    packed pairs), R = 1..4 and K = 1..16 (every chunk split: 1 + 0, 2 + 2 +
+    2 + 1 ...; m = 6: a unit launch plus a general one), here plus a word tail.
+    1600 blocks run the workgroups' column loop more than once (the grid is
+    one resident round).  Encode and a decode of up to m erasures against the
+    reference library."""
+    import torch
+    if blocks > 3 and (k, m) not in [(10, 4), (16, 4), (5, 3)]:
+        pytest.skip("large sizes on three shapes")
+    monkeypatch.delenv("ECGPU_WIDE", raising=False)
+    monkeypatch.delenv("ECGPU_NIB16", raising=False)
+    monkeypatch.delenv("ECGPU_WIDE_UNITS", raising=False)
+    monkeypatch.setenv("ECGPU_WIDE_PIPE", pipe)
+    ref = _ref_nsa()
+    rng = np.random.default_rng(31 * w + 7 * k + m + blocks)
+    if structure == "vandermonde":
+        M = list(ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w))
+    else:
+        hi = (1 << w) - 1
+        M = [int(x) for x in rng.integers(0, hi, k * m, dtype=np.uint64, endpoint=True)]
+        for i in rng.choice(k * m, size=(k * m) // 4, replace=False):
+            M[int(i)] = int(rng.integers(0, 2))
+        M = [x if x < 2**31 else x - 2**32 for x in M]
+    size = 4096 * blocks + 2 * (w // 8)  # whole column blocks + a word tail
+    data = [rng.integers(0, 256, size + 64, dtype=np.uint8) for _ in range(k)]
+    coding = [np.zeros(size + 64, np.uint8) for _ in range(m)]
+    ref._Z22jerasure_matrix_encodeiiiPiPPcS1_i(k, m, w, _cints(M), _cptrs(data), _cptrs(coding), size)
+    dd = [torch.from_numpy(a[:size].copy()).to(gpu) for a in data]
+    dc = [torch.full((size,), 0x5A, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    ec.jerasure.jerasure_matrix_encode(k, m, w, M, dd, dc, size)
+    torch.cuda.synchronize()
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
+    if structure != "vandermonde":
+        return  # random matrices need not be MDS
+    er = sorted(int(x) for x in rng.choice(k + m, size=min(m, k + m - 1), replace=False))
+    for e in er:
+        (dd + dc)[e].fill_(0)
+    assert ec.jerasure.jerasure_matrix_decode(k, m, w, M, 0, er, dd, dc, size) == 0
+    torch.cuda.synchronize()
+    for j in range(k):
+        assert np.array_equal(dd[j].cpu().numpy(), data[j][:size]), j
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
+
+
 @pytest.mark.parametrize("w", [16, 32])
 def test_wide_word_region_ops_device(ec, gpu, w):
     import torch

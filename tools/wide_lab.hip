@@ -6,7 +6,7 @@
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I erasure_coding_test_amd/csrc \
 //     tools/wide_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp erasure_coding_test_amd/csrc/matrix_host.cpp -o tools/wide_lab.bin
-//   tools/wide_lab.bin [--w 32] [--k 10] [--m 4] [--mib 64] [--rounds 7] [--reps 10] [--only name]
+//   tools/wide_lab.bin [--w 32] [--k 10] [--m 4] [--mib 64] [--rounds 7] [--reps 10] [--only name,name]
 //
 // Prints one JSON line per variant: median / min us and GB/s of (k+m)*S.
 #include <hip/hip_runtime.h>
@@ -18,6 +18,7 @@
 #include <functional>
 #include <random>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "gf_host.hpp"
@@ -357,6 +358,26 @@ constexpr unsigned split_lds(int K) {
 
 }  // namespace lab
 
+// production's pipelined wide kernel (gf_apply_wide_pipe<K, 4, mode>) for the
+// lab's K: 5, 7, 8, 10, 11, 12
+const void* pipe_fn(int K, int mode) {
+  auto pick = [&](auto k) -> const void* {
+    constexpr int kK = decltype(k)::value;
+    return mode == kPipeW16      ? reinterpret_cast<const void*>(&gf_apply_wide_pipe<kK, 4, kPipeW16>)
+           : mode == kPipeW32Unit ? reinterpret_cast<const void*>(&gf_apply_wide_pipe<kK, 4, kPipeW32Unit>)
+                                  : reinterpret_cast<const void*>(&gf_apply_wide_pipe<kK, 4, kPipeW32>);
+  };
+  switch (K) {
+    case 5: return pick(std::integral_constant<int, 5>{});
+    case 7: return pick(std::integral_constant<int, 7>{});
+    case 8: return pick(std::integral_constant<int, 8>{});
+    case 10: return pick(std::integral_constant<int, 10>{});
+    case 11: return pick(std::integral_constant<int, 11>{});
+    case 12: return pick(std::integral_constant<int, 12>{});
+    default: return nullptr;
+  }
+}
+
 struct Variant {
   std::string name;
   const void* fn;
@@ -444,6 +465,8 @@ int main(int argc, char** argv) {
   vs.push_back({name, reinterpret_cast<const void*>(&lab::nib_split<__VA_ARGS__>), lab::split_lds<4, 1, true>(K)})
   if (w == 32) {
     vs.push_back({"prod_u0", reinterpret_cast<const void*>(&gf_apply_wide_nib<4>), unsigned(nib_lds_bytes(K, 4, 0))});
+    if (const void* f = pipe_fn(K, kPipeW32); f && (S / 16) % kBlock == 0)
+      vs.push_back({"prod_pipe_u0", f, unsigned(nib_lds_bytes(K, 4, 0))});
     V("u0_c8", 4, 0, true, 8, 1, 1);
     V("u0_c4_h4", 4, 0, true, 4, 4, 1);
     V("u0_c4_h2", 4, 0, true, 4, 2, 1);
@@ -460,6 +483,15 @@ int main(int argc, char** argv) {
       VU("u1_c5_h4", 4, 1, true, 5, 4, 1);
       VU("u1_c3_h2", 4, 1, true, 3, 2, 1);
       VU("u1_c2_h4", 4, 1, true, 2, 4, 1);
+      if (const void* f = pipe_fn(K, kPipeW32Unit); f && (S / 16) % kBlock == 0) {
+        vs.push_back({"prod_pipe", f, unsigned(nib_lds_bytes(K, 4, 1))});
+        if (K == 10) {
+          vs.push_back({"pipe_wpe5", reinterpret_cast<const void*>(&gf_apply_wide_pipe<10, 4, kPipeW32Unit, 5>),
+                        unsigned(nib_lds_bytes(K, 4, 1))});
+          vs.push_back({"pipe_wpe6", reinterpret_cast<const void*>(&gf_apply_wide_pipe<10, 4, kPipeW32Unit, 6>),
+                        unsigned(nib_lds_bytes(K, 4, 1))});
+        }
+      }
     }
   } else {
     const unsigned l16 = unsigned(K * nib16_source_bytes(4));
@@ -475,6 +507,9 @@ int main(int argc, char** argv) {
       vs.push_back({"prod_nib16_4_grid" + std::to_string(b), reinterpret_cast<const void*>(&gf_apply_wide_nib16<4>), l16, b});
     for (int b : {2, 3, 4})
       vs.push_back({"n16_c2_g2_grid" + std::to_string(b), reinterpret_cast<const void*>(&lab::nib16v<4, 2, 2>), l16, b});
+    if (const void* f = pipe_fn(K, kPipeW16); f && (S / 16) % kBlock == 0)
+      for (int b : {0, 3, 4})
+        vs.push_back({b ? "prod_pipe16_grid" + std::to_string(b) : "prod_pipe16", f, l16, b});
     if (unit_rc) {
       const unsigned lu = unsigned((K - 1) * nib16_source_bytes(3));
       for (int b : {0, 2, 3, 4}) {
@@ -548,7 +583,15 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   for (int rd = 0; rd < rounds; ++rd)
     for (size_t i = 0; i < vs.size(); ++i) {
-      if (!only.empty() && vs[i].name.find(only) == std::string::npos && i != 0) continue;
+      if (!only.empty() && i != 0) {  // --only a,b,c: names containing any of them
+        bool hit = false;
+        for (size_t p0 = 0; p0 <= only.size();) {
+          const size_t p1 = std::min(only.find(',', p0), only.size());
+          hit = hit || vs[i].name.find(only.substr(p0, p1 - p0)) != std::string::npos;
+          p0 = p1 + 1;
+        }
+        if (!hit) continue;
+      }
       for (int q = 0; q < 2; ++q) launch(vs[i], a);  // warm
       for (int q = 0; q < reps; ++q) {
         CK(hipEventRecord(e0, nullptr));

@@ -1405,7 +1405,10 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
 
 // ------------------------------------- wide words, pipelined loads ----
 // The two nibble kernels above with compile-time K and software-pipelined
-// shard loads (production for launches of whole 256-column blocks).  The K
+// shard loads.  Production where it measured faster: launches of whole
+// 256-column blocks in the w = 32 unit form with 7-10 sources
+// (ecgpu_runtime.hip plan_launch_wide; ECGPU_WIDE_PIPE=2 takes it for every
+// whole-block launch of every mode, for tests and A/B).  The K
 // sources of a column are NCH (even) chunks of CH, and the chunk sequence is
 // double-buffered across the workgroup's column blocks: chunk c + 1's loads
 // (after the last chunk, the next block's chunk 0) are issued before chunk
@@ -1415,9 +1418,10 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
 // for the chunk it is about to look up.  The runtime-K kernels load a chunk
 // and wait for it before any lookup, leaving the wait to other waves to
 // hide (a first pipelined form with conditional loads got vmcnt(0) before
-// every chunk and ran slower).  RS(10,4) 64 MiB, tools/wide_lab.hip in one
-// process: w = 32 195 -> 184-187 us, w = 16 175 -> 170 us
-// (profiles/r03_wide_lab.jsonl, run "r03 pipe static").
+// every chunk and ran slower).  RS(K,4) 64 MiB, tools/wide_lab.hip in one
+// process, unit form: K = 7 148 -> 139 us, K = 8 162 -> 149, K = 10 195 ->
+// 184-191; K = 5, 11, 12, the general w = 32 form and w = 16 within +-3 %
+// (profiles/r03_wide_lab.jsonl, runs "r03 pipe ...").
 enum WidePipeMode : int { kPipeW32 = 0, kPipeW32Unit = 1, kPipeW16 = 2 };
 
 template <int K, int MODE>

@@ -80,10 +80,73 @@ __global__ __launch_bounds__(256) void enc_early0(ApplyArgs a) {
 #pragma unroll
   for (int r = 1; r < R; ++r) store16t<1>(dp[r], col, acc[r - 1]);
 }
+// Persistent, software-pipelined form (round 3 lab): a resident round of
+// workgroups walks the (stripe, column block) items; a column's K sources are
+// two chunks, double-buffered across items -- chunk 1's loads (and the next
+// item's chunk 0) are in flight while the previous chunk is multiplied.  All
+// loads and stores unconditional (the last prefetch re-reads the current
+// item), so the wait counts are static.
+template <int K, int R, int UNITS>
+__global__ __launch_bounds__(256) void enc_pipe(ApplyArgs a, int stripes) {
+  constexpr int CH = (K + 1) / 2;
+  const int64_t nblk = a.nvec / 256, items = nblk * stripes, g = gridDim.x;
+  int64_t it = blockIdx.x;
+  if (it >= items) return;
+  const kconst_u32* ptab = (const kconst_u32*)a.ptab;
+  auto load = [&](u32x4 (&x)[CH], int64_t item, int c) {
+    const int64_t s = item / nblk, col = (item - s * nblk) * 256 + threadIdx.x;
+    const uint8_t* const* sp = a.src + s * a.src_stride;
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      if (c * CH + u < K) x[u] = load16t<1>(kload(sp, c * CH + u), col);
+  };
+  u32x4 b0[CH], b1[CH];
+  load(b0, it, 0);
+  for (;;) {
+    const int64_t nx = it + g < items ? it + g : it;
+    Xacc xa[R][4];
+    auto apply = [&](const u32x4 (&x)[CH], int c) {
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int j = c * CH + u;
+        if (j >= K) break;
+        Sel3 sl[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sl[q] = sel3(x[u][q]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (is_unit<UNITS>(r, j)) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xa[r][q].add(x[u][q]);
+          } else {
+            const kconst_u32* t = ptab + (r * K + j) * kP3Words;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) mac3(xa[r][q], t, sl[q]);
+          }
+        }
+      }
+    };
+    load(b1, it, 1);
+    apply(b0, 0);
+    load(b0, nx, 0);
+    apply(b1, 1);
+    const int64_t s = it / nblk, col = (it - s * nblk) * 256 + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      u32x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = xa[r][q].value();
+      store16t<1>(a.dst[s * a.dst_stride + a.row0 + r], col, o);
+    }
+    if (nx == it) break;
+    it = nx;
+  }
+}
 }  // namespace lab
 
 bool g_early0 = false;  // --early0 1: skew mode also times lab::enc_early0 on every slab
 bool g_vec2 = false;    // --vec2 1: ... and the production body with two columns per lane (VEC = 2)
+bool g_dense = false;   // --dense 1: a C4-like dense 4 x 10 map (no 0 / 1 coefficients) instead of the encode
 
 struct Variant {
   std::string name;
@@ -139,6 +202,7 @@ int main(int argc, char** argv) {
     else if (f == "--kib") kib = std::atoi(argv[i + 1]);
     else if (f == "--early0") g_early0 = std::atoi(argv[i + 1]) != 0;
     else if (f == "--vec2") g_vec2 = std::atoi(argv[i + 1]) != 0;
+    else if (f == "--dense") g_dense = std::atoi(argv[i + 1]) != 0;
     else if (f == "--skews") {
       std::string v = argv[i + 1];
       size_t p = 0;
@@ -161,6 +225,10 @@ int main(int argc, char** argv) {
   constexpr int k = 10, m = 4;
   const size_t S = size_t(4) << 20, stride = S + (10 << 10);
   int* M = vandermonde_coding_matrix(k, m, 8);
+  if (g_dense) {
+    std::mt19937 gm(4);
+    for (int i = 0; i < k * m; ++i) M[i] = 2 + int(gm() % 254);  // no 0 / 1: every term multiplies (C4's decode rows)
+  }
   std::vector<uint32_t> ptab(size_t(m) * k * kP3Words);
   for (int r = 0; r < m; ++r)
     for (int j = 0; j < k; ++j) build_p3(M[r * k + j], &ptab[(size_t(r) * k + j) * kP3Words]);
@@ -202,10 +270,20 @@ int main(int argc, char** argv) {
   a.K = k;
   a.R = m;
   a.nt = 1;
-  constexpr int U = kUnitCol0 | kUnitRow0;
-  std::vector<Variant> vs = {
+  constexpr int U = kUnitCol0 | kUnitRow0, N = kUnitNone;
+  // bs < 0: the persistent pipelined form (a resident round of |bs| workgroups per CU)
+  std::vector<Variant> vs = g_dense ? std::vector<Variant>{
+      {"prod_dense_cap3", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 3},
+      {"dense_cap4", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 4},
+      {"dense_uncapped", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 0},
+      {"pipe_dense_r3", reinterpret_cast<const void*>(&lab::enc_pipe<k, m, N>), -3, 0},
+      {"pipe_dense_r4", reinterpret_cast<const void*>(&lab::enc_pipe<k, m, N>), -4, 0},
+      {"pipe_dense_r5", reinterpret_cast<const void*>(&lab::enc_pipe<k, m, N>), -5, 0},
+  } : std::vector<Variant>{
       {"prod_bs256_cap3", reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>), 256, 3},
       {"bs256_cap4", reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>), 256, 4},
+      {"pipe_r3", reinterpret_cast<const void*>(&lab::enc_pipe<k, m, U>), -3, 0},
+      {"pipe_r4", reinterpret_cast<const void*>(&lab::enc_pipe<k, m, U>), -4, 0},
       {"bs256_cap2", reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>), 256, 2},
       {"bs512_cap1", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 512>), 512, 1},
       {"bs512_cap2", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 512>), 512, 2},
@@ -213,6 +291,8 @@ int main(int argc, char** argv) {
       {"bs1024_cap1", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 1024>), 1024, 1},
       {"bs1024_cap2", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 1024>), 1024, 2},
   };
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   int dev = 0, lds_cu = 0;
   CK(hipGetDevice(&dev));
   CK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
@@ -223,7 +303,12 @@ int main(int argc, char** argv) {
   };
   auto launch = [&](const Variant& v) {
     ApplyArgs args = a;
-    void* kargs[] = {&args};
+    int ns = stripes;
+    void* kargs[] = {&args, &ns};
+    if (v.bs < 0) {  // persistent: one resident round, items = column blocks x stripes
+      CK(hipLaunchKernel(v.fn, dim3(unsigned(-v.bs * cus)), dim3(256), kargs, 0, nullptr));
+      return;
+    }
     const dim3 grid(unsigned((a.nvec + v.bs - 1) / v.bs), unsigned(stripes));
     CK(hipLaunchKernel(v.fn, grid, dim3(unsigned(v.bs)), kargs, lds_of(v), nullptr));
   };
@@ -242,7 +327,7 @@ int main(int argc, char** argv) {
         uint8_t e = 0;
         for (int j = 0; j < k; ++j) e ^= uint8_t(single_multiply(M[r * k + j], col[j], 8));
         uint8_t o;
-        CK(hipMemcpy(&o, hd[size_t(s * m + r)] + b, 1, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(&o, hd[size_t(s * m + r)] + b, 1, hipMemcpyDeviceToHost));  // (dense: M was overwritten above)
         if (o != e) {
           std::fprintf(stderr, "production launch disagrees with the host\n");
           return 1;

@@ -1003,7 +1003,8 @@ def test_wide_word_unit_structured_launches(ec, gpu, monkeypatch, w, nib16, unit
         assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
 
 
-_PIPE_SHAPES = [(1, 1), (2, 2), (3, 4), (5, 3), (6, 4), (7, 2), (10, 4), (12, 4), (13, 3), (16, 4), (10, 6)]
+_PIPE_SHAPES = [(1, 1), (2, 2), (3, 4), (4, 1), (5, 3), (6, 4), (7, 2), (8, 3), (9, 2), (10, 4), (11, 4), (12, 4),
+                (13, 3), (14, 2), (15, 3), (16, 4), (10, 6)]
 
 
 @pytest.mark.parametrize("w", [16, 32])

@@ -73,7 +73,8 @@ def parse(argv=None):
     ap.add_argument("--nt", type=int, default=1, help="non-temporal loads/stores")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the per-config block (C2 / C3 / C4 / C5 launches, N = 1 only)")
+                    help="skip the per-config block (C2 / C3 / C4 / C5 launches; run by every rank on its own GPU "
+                         "at any N)")
     ap.add_argument("--e2e-stripes", type=int, default=24,
                     help="pinned host stripes for the PCIe-inclusive e2e rate on rank 0 (0 = skip)")
     ap.add_argument("--spawn-selftest", action="store_true",
@@ -196,6 +197,42 @@ def gather(obj, world: int) -> list:
     return out
 
 
+def device_identity(N, local: int) -> dict:
+    """The physical GPU a rank runs on: its PCI bus id (hipDeviceGetPCIBusId,
+    through the library) and UUID, so an N > 1 line proves its ranks used N
+    distinct devices."""
+    import ctypes
+
+    import torch
+    buf = ctypes.create_string_buffer(64)
+    bus = buf.value.decode() if N.lib.ecgpu_device_pci_bus_id(local, buf, len(buf)) == 0 else None
+    try:
+        uuid = str(torch.cuda.get_device_properties(local).uuid)
+    except Exception:  # noqa: BLE001 -- informative only
+        uuid = None
+    return {"pci_bus_id": bus, "uuid": uuid}
+
+
+def distinct_devices(per_rank: list, rehearsal: bool):
+    """(ok, note): every rank of a real N > 1 run must sit on its own GPU
+    (PCI bus id, else UUID).  A rehearsal puts every rank on cuda:0 on
+    purpose and is exempt.  Pure: tested on CPU."""
+    if len(per_rank) <= 1:
+        return True, "one rank"
+    if rehearsal:
+        return True, "rehearsal: every rank on cuda:0 by design (ECGPU_BENCH_ONE_DEVICE=1), not checked"
+    seen = {}
+    for p in per_rank:
+        key = p.get("pci_bus_id") or p.get("uuid")
+        if key is None:
+            return False, f"rank {p.get('rank')} reported no PCI bus id or UUID: distinct devices unproven"
+        seen.setdefault(key, []).append(p.get("rank"))
+    dups = {k: v for k, v in seen.items() if len(v) > 1}
+    if dups:
+        return False, "ranks share a GPU: " + "; ".join(f"ranks {v} on {k}" for k, v in sorted(dups.items()))
+    return True, f"{len(seen)} ranks on {len(seen)} distinct GPUs (PCI bus ids)"
+
+
 def stripes_for_rank(total: int, rank: int, world: int) -> list:
     """Global stripe ids owned by a rank: round-robin."""
     return list(range(rank, total, world))
@@ -229,18 +266,53 @@ def host_has_avx2() -> bool:
 HOST_THREAD_CAP = 16  # the GPU box's CPU share per GPU (16 per one-GPU lease)
 
 
-def host_cpus() -> list:
-    """CPUs this process may run on (affinity), at most HOST_THREAD_CAP of them:
-    the box's per-GPU CPU share, whatever the machine's total core count."""
+def cgroup_cpu_quota(root: str = "/sys/fs/cgroup"):
+    """CPUs' worth of run time the cgroup grants this process (cgroup v2
+    cpu.max, else v1 cfs quota / period), or None when unlimited / unknown.
+    A one-GPU lease shows the whole machine in its affinity mask but is
+    throttled to its share; threads beyond the quota would only queue."""
     try:
-        cpus = sorted(os.sched_getaffinity(0))
+        with open(os.path.join(root, "cpu.max")) as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else max(1, int(quota) // max(1, int(period)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open(os.path.join(root, "cpu", "cpu.cfs_quota_us")) as f:
+            quota = int(f.read())
+        with open(os.path.join(root, "cpu", "cpu.cfs_period_us")) as f:
+            period = int(f.read())
+        return None if quota <= 0 else max(1, quota // max(1, period))
+    except (OSError, ValueError):
+        return None
+
+
+def affinity_cpus() -> list:
+    try:
+        return sorted(os.sched_getaffinity(0))
     except AttributeError:
-        cpus = list(range(os.cpu_count() or 1))
-    return cpus[:HOST_THREAD_CAP] or [0]
+        return list(range(os.cpu_count() or 1))
+
+
+def host_cpus(cap=HOST_THREAD_CAP) -> list:
+    """CPUs this process may run on (affinity), at most `cap` of them (the
+    per-GPU share by default) and at most the cgroup's CPU quota."""
+    cpus = affinity_cpus()
+    quota = cgroup_cpu_quota()
+    n = len(cpus) if cap is None else min(cap, len(cpus))
+    if quota is not None:
+        n = min(n, quota)
+    return cpus[:max(1, n)] or [0]
+
+
+def all_host_cpus() -> list:
+    """Every CPU this process may run on (SURVEY.md §8d "all host cores"):
+    the affinity mask, bounded by the cgroup quota."""
+    return host_cpus(cap=None)
 
 
 # ------------------------------------------------------------ CPU baseline ----
-def cpu_baseline(seconds: float, host_stripe, k, m, erasures, threads: int = 1, o3: bool = False):
+def cpu_baseline(seconds: float, host_stripe, k, m, erasures, threads: int = 1, o3: bool = False, cpus=None):
     """Reference CPU path on the host cores: oracle/_ref (the reference's own
     src/erasure_coding compiled -O2, or -O3 -march=x86-64-v3) if shipped, else
     our C restatement (oracle/ec_oracle.c).  Bounded sample of the same
@@ -272,7 +344,7 @@ def cpu_baseline(seconds: float, host_stripe, k, m, erasures, threads: int = 1, 
     for j in range(k):
         data[j][:S] = host_stripe[j]
     coding = alloc_shards(m, S)
-    cpus = host_cpus()
+    cpus = host_cpus() if cpus is None else cpus
     threads = max(1, min(threads, len(cpus)))
     ranges, off = [], 0
     for t in range(threads):
@@ -316,7 +388,10 @@ def cpu_baseline(seconds: float, host_stripe, k, m, erasures, threads: int = 1, 
     flags = "-O3 -march=x86-64-v3" if o3 else "-O2"
     src = f"reference src/erasure_coding compiled g++ {flags}" if o.kind == "reference" else "oracle/ec_oracle.c -O2"
     step = f"RS({k},{m}) {S >> 20} MiB stripe encode" + (f" + decode of erasures {set(erasures)}" if erasures else "")
-    cap = f", capped at {HOST_THREAD_CAP} = the box's per-GPU CPU share" if threads > 1 else ""
+    cap = ""
+    if threads > 1:
+        cap = (f" (of {len(affinity_cpus())} in the affinity mask, cgroup quota "
+               f"{cgroup_cpu_quota() or 'none'}; the per-GPU share is {HOST_THREAD_CAP})")
     return ({"value": round(gib / el, 4), "unit": "GiB/s", "cores": threads, "kind": o.kind,
              "sample": f"{iters} x ({step}) on stripe 0 of the GPU slab, {threads} thread(s) pinned one per CPU{cap}, "
                        f"splitting byte ranges like client_main.cpp:1074-1164, {el:.1f} s, {src}, "
@@ -659,15 +734,23 @@ def selftest_main(args):
     rank, local, world = dist_setup()
     barrier(world)
     t = max_over_ranks(float(rank + 1), world)
-    per_rank = gather({"rank": rank, "local_rank": local, "world": world, "pid": os.getpid()}, world)
+    # a stand-in device identity per rank (ECGPU_SELFTEST_SAME_BUS=1: every
+    # rank claims one device, which the distinct-device check must fail)
+    bus = "selftest:00" if os.environ.get("ECGPU_SELFTEST_SAME_BUS") == "1" else f"selftest:{local:02d}"
+    per_rank = gather({"rank": rank, "local_rank": local, "world": world, "pid": os.getpid(), "pci_bus_id": bus},
+                      world)
+    devices_ok, devices_note = distinct_devices(per_rank, os.environ.get("ECGPU_BENCH_ONE_DEVICE") == "1")
     if rank == 0:
         print(json.dumps({"selftest": True, "n_gpus": world, "max_over_ranks": t, "per_rank": per_rank,
-                          "stripes": {r: global_stripe_ids(2, r, world) for r in range(world)}}), flush=True)
+                          "stripes": {r: global_stripe_ids(2, r, world) for r in range(world)},
+                          "distinct_devices_ok": devices_ok, "distinct_devices": devices_note}), flush=True)
+        if not devices_ok:
+            print(f"bench.py: {devices_note}", file=sys.stderr, flush=True)
     barrier(world)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
-    return 0
+    return 0 if devices_ok else 1
 
 
 def main(argv=None):
@@ -800,7 +883,7 @@ def main(argv=None):
         configs = config_block(E, N, dev, stream, kind, bool(args.nt), main_entries)
 
     enc_frac = enc_bytes / (enc_ms / 1e3) / 1e9 / HBM_PEAK_GBS
-    mine = {"rank": rank, "device": local, "elapsed_s": round(elapsed, 6),
+    mine = {"rank": rank, "device": local, **device_identity(N, local), "elapsed_s": round(elapsed, 6),
             "encode_median_ms": round(enc_ms, 4), "encode_frac": round(enc_frac, 4),
             "decode_median_ms": round(dec_ms, 4) if dec_ms is not None else None,
             "decode_frac": (round(dec_bytes / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if dec_ms is not None
@@ -813,17 +896,26 @@ def main(argv=None):
                            for name, e in configs.items()}
     per_rank = gather(mine, world)
     ok = all(p["parity_ok"] for p in per_rank)
+    devices_ok, devices_note = distinct_devices(per_rank, rehearsal)
     barrier(world)  # every rank's GPU work is done: the CPU baseline below runs alone
 
     workload = C["workload"].format(B=B)
     cpu_ok = None
     if rank == 0:
-        cpu = cpu_all = cpu_o3 = None
+        cpu = cpu_share = cpu_all = cpu_o3 = None
         if host_stripe is not None:
             cpu, cpu_ok = cpu_baseline(args.cpu_seconds, host_stripe, k, m, erasures)
-            cpu_all, ok_all = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_stripe, k, m, erasures,
-                                           threads=HOST_THREAD_CAP)
-            cpu_ok = cpu_ok and ok_all
+            share = host_cpus()
+            cpu_share, ok_share = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_stripe, k, m, erasures,
+                                               threads=len(share), cpus=share)
+            cpu_ok = cpu_ok and ok_share
+            every = all_host_cpus()
+            if len(every) > len(share):  # a whole host (the 8-GPU node): every core it gives us
+                cpu_all, ok_all = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_stripe, k, m, erasures,
+                                               threads=len(every), cpus=every)
+                cpu_ok = cpu_ok and ok_all
+            else:  # a one-GPU lease: its share is all there is
+                cpu_all = dict(cpu_share, note="the per-GPU share is every CPU this process may use here")
             from oracle.oracle import REFERENCE_O3_SO
             if host_has_avx2() and os.path.exists(REFERENCE_O3_SO):
                 cpu_o3, ok_o3 = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_stripe, k, m, erasures, o3=True)
@@ -831,6 +923,8 @@ def main(argv=None):
         # about 1.5 GiB of pinned host memory at most (C3: 24 stripes, C5: 6)
         e2e_n = min(args.e2e_stripes, max(2, (3 << 29) // ((k + m) * S)))
         e2e = e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes=e2e_n) if args.e2e_stripes > 0 else None
+        e2e_ok = (None if not e2e else
+                  bool(e2e["encode"]["parity_ok"] and e2e.get("decode", {}).get("rebuilt_ok", True)))
         achieved = enc_bytes / (enc_ms / 1e3) / 1e9
         wkey = f"{args.config}:{B}"
         kernel_id = N.lib.ecgpu_build_id(1).decode()
@@ -877,15 +971,22 @@ def main(argv=None):
             "per_rank": per_rank,
             "configs": configs,
             "cpu_baseline": cpu,
+            "cpu_baseline_per_gpu_share": cpu_share,
             "cpu_baseline_all_cores": cpu_all,
             "cpu_baseline_o3": cpu_o3,
             "e2e": e2e,
             "selfcheck_parity_ok": ok,
             "selfcheck_vs_reference_cpu": cpu_ok,
+            "e2e_ok": e2e_ok,
+            "distinct_devices_ok": devices_ok,
+            "distinct_devices": devices_note,
             "build_id": {"library": N.lib.ecgpu_build_id(0).decode(), "kernels": kernel_id},
         }
         print(json.dumps(out), flush=True)
-        if e2e and not (e2e["encode"]["parity_ok"] and e2e.get("decode", {}).get("rebuilt_ok", True)):
+        if e2e_ok is False:
+            ok = False
+        if not devices_ok:
+            print(f"bench.py: {devices_note}", file=sys.stderr, flush=True)
             ok = False
     barrier(world)
     if world > 1:

@@ -54,6 +54,8 @@ SIGNATURES = {
     "ecgpu_galois_get_ilog_table": (c_int_p, [c_int]),
     "ecgpu_galois_shift_multiply": (c_int, [c_int, c_int, c_int]),
     "ecgpu_galois_shift_inverse": (c_int, [c_int, c_int]),
+    "ecgpu_galois_create_split_w8_tables": (c_int, []),
+    "ecgpu_galois_split_w8_multiply": (c_int, [c_int, c_int]),
     "ecgpu_reed_sol_vandermonde_coding_matrix": (c_void_p, [c_int, c_int, c_int]),
     "ecgpu_reed_sol_extended_vandermonde_matrix": (c_void_p, [c_int, c_int, c_int]),
     "ecgpu_reed_sol_big_vandermonde_distribution_matrix": (c_void_p, [c_int, c_int, c_int]),
@@ -98,6 +100,7 @@ SIGNATURES = {
     "ecgpu_jerasure_get_stats": (c_int, [c_double_p]),
     "ecgpu_plan_create": (c_void_p, [c_int, c_int, c_int_p, c_int]),
     "ecgpu_plan_bind": (c_int, [c_void_p, c_int, c_void_pp, c_void_pp, c_int64]),
+    "ecgpu_plan_check_buffers": (c_int, [c_int, c_int, c_int, c_void_pp, c_void_pp, c_int64]),
     "ecgpu_plan_set_kernel": (c_int, [c_void_p, c_int, c_int]),
     "ecgpu_plan_launch": (c_int, [c_void_p, c_void_p]),
     "ecgpu_plan_destroy": (None, [c_void_p]),
@@ -116,6 +119,7 @@ SIGNATURES = {
     "ecgpu_pipeline_group_drain": (c_int, [c_void_p]),
     "ecgpu_pipeline_group_size": (c_int, [c_void_p]),
     "ecgpu_pipeline_group_destroy": (None, [c_void_p]),
+    "ecgpu_device_pci_bus_id": (c_int, [c_int, c_char_p, c_int]),
     "ecgpu_host_register": (c_int, [c_void_p, c_int64]),
     "ecgpu_host_unregister": (c_int, [c_void_p]),
     "ecgpu_accum_create": (c_void_p, [c_int, c_int64, c_int]),

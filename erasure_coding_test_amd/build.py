@@ -15,8 +15,10 @@ line and the bytes of its source and every header (stored beside it as
 <object>.key), so neither a touched-but-unchanged file nor a stale object with
 a newer mtime decides.  The library carries two IDs (ecgpu_build_id):
   0  the whole library: every source and header under csrc/ + ecgpu.h + flags
+     + both compilers' --version
   1  the coding kernels and their dispatch (gf_kernels / gf_spec / the runtime
-     and planner that pick grids, engines and cache policies) + HIP flags --
+     and planner that pick grids, engines and cache policies) + HIP flags +
+     hipcc --version --
      the identity a rocprofv3 PMC record of a launch is valid for
      (profiles/summarize.py writes it, bench.py checks it).
 """
@@ -39,12 +41,12 @@ ARCH = os.environ.get("ECGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 
-HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp"]
+HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp", "contract_host.cpp"]
 # (source, object, extra flags): the specialised kernel table is split into
 # one translation unit per output-row count so the four compile in parallel
 HIP_UNITS = [(f, f + ".o", []) for f in ("ecgpu_runtime.hip", "accum.hip", "pipeline.hip", "packets.hip")] + [
     ("gf_spec.hip", f"gf_spec_r{r}.hip.o", [f"-DECGPU_SPEC_R={r}"]) for r in (1, 2, 3, 4)]
-HDRS = ["gf_host.hpp", "host_sync.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp", "gf_spec.hpp",
+HDRS = ["buffer_contract.hpp", "gf_host.hpp", "host_sync.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp", "gf_spec.hpp",
         "runtime.hpp"]
 DROPIN_SRCS = ["jerasure_dropin.cpp", "jerasure_surface.cpp"]
 
@@ -86,18 +88,36 @@ def _digest(parts, files) -> str:
     return h.hexdigest()
 
 
+_versions: dict = {}
+
+
+def toolchain(compiler: str) -> str:
+    """`<compiler> --version` (cached per process): part of every object key
+    and build ID, so a compiler change rebuilds everything and invalidates PMC
+    records taken on the old code."""
+    if compiler not in _versions:
+        try:
+            r = subprocess.run([compiler, "--version"], capture_output=True, text=True, timeout=60)
+            _versions[compiler] = r.stdout.strip() or f"{compiler}: no version output"
+        except (OSError, subprocess.SubprocessError) as ex:
+            _versions[compiler] = f"{compiler}: {type(ex).__name__}"
+    return _versions[compiler]
+
+
 def build_ids() -> dict:
     """{'build': ..., 'kernels': ...}: 16-hex content IDs (see module doc)."""
     all_srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
                       if f.endswith((".hip", ".cpp", ".hpp")) and f != "diag_kernels.hip")
-    return {"build": _digest([ARCH] + CXXFLAGS + HIPFLAGS, all_srcs + [os.path.join(INCLUDE, "ecgpu.h")])[:16],
-            "kernels": _digest([ARCH] + HIPFLAGS, [os.path.join(CSRC, f) for f in KERNEL_ID_SRCS])[:16]}
+    hip, cxx = toolchain(HIPCC), toolchain(CXX)
+    return {"build": _digest([ARCH, hip, cxx] + CXXFLAGS + HIPFLAGS,
+                             all_srcs + [os.path.join(INCLUDE, "ecgpu.h")])[:16],
+            "kernels": _digest([ARCH, hip] + HIPFLAGS, [os.path.join(CSRC, f) for f in KERNEL_ID_SRCS])[:16]}
 
 
 def _stale(target, deps, cmd=()):
     """True when `target` must be rebuilt; records the new key when so (the
     caller builds it next; a failed build raises before anything reads it)."""
-    key = _digest(list(cmd), [d for d in deps if os.path.exists(d)])
+    key = _digest(list(cmd) + ([toolchain(cmd[0])] if cmd else []), [d for d in deps if os.path.exists(d)])
     stamp = target + ".key"
     try:
         with open(stamp) as f:

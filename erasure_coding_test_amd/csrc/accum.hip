@@ -19,6 +19,7 @@
 #include <utility>
 #include <vector>
 
+#include "buffer_contract.hpp"
 #include "ecgpu.h"
 #include "gf_host.hpp"
 #include "matrix_host.hpp"
@@ -126,7 +127,7 @@ ECGPU_API int ecgpu_accum_add(ecgpu_accum* a, const char* block, const int* coef
   if (!a || !block || !coefs) return fail(ECGPU_ERR_ARG, "ecgpu_accum_add: bad arguments");
   if (int rc = accum_sync(a)) return rc;  // after every earlier asynchronous add
   DeviceGuard g(a->device);
-  const int rc = execute(accum_op(a, block, coefs), a->size);
+  const int rc = execute(accum_op(a, block, coefs), a->size, "ecgpu_accum_add");
   if (rc != ECGPU_OK) return rc;
   for (int i = 0; i < a->m; ++i)
     if (coefs[i] & 0xFF) a->init[i] = 1;
@@ -146,6 +147,9 @@ ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int
   bool any = false;
   for (int i = 0; i < a->m; ++i) any |= (coefs[i] & 0xFF) != 0;
   if (!any || a->size == 0) return ECGPU_OK;
+  // a block that shares bytes with an accumulator it updates: rejected
+  // before anything is queued (buffer_contract.hpp)
+  if (int rc = check_op_buffers("ecgpu_accum_add_async", accum_op(a, block, coefs), a->size)) return rc;
   if (int rc = accum_async_init(a)) return rc;
   DeviceGuard g(a->device);
   bool on_dev = false;
@@ -174,7 +178,7 @@ ECGPU_API int ecgpu_accum_add_async(ecgpu_accum* a, const char* block, const int
     // classifies and maps host memory itself -- so it gets the caller's
     // pointer, not the device alias of a pinned block
     if (int rc = accum_sync(a)) return rc;
-    if (int rc = execute(in_place ? accum_op(a, block, coefs) : op, a->size)) return rc;
+    if (int rc = execute(in_place ? accum_op(a, block, coefs) : op, a->size, "ecgpu_accum_add_async")) return rc;
   }
   for (int i = 0; i < a->m; ++i)
     if (coefs[i] & 0xFF) a->init[i] = 1;

@@ -94,6 +94,8 @@ ECGPU_API int* ecgpu_galois_get_log_table(int w) { return log_table(w); }
 ECGPU_API int* ecgpu_galois_get_ilog_table(int w) { return ilog_table(w); }
 ECGPU_API int ecgpu_galois_shift_multiply(int a, int b, int w) { return shift_multiply(a, b, w); }
 ECGPU_API int ecgpu_galois_shift_inverse(int a, int w) { return shift_inverse(a, w); }
+ECGPU_API int ecgpu_galois_create_split_w8_tables(void) { return create_split_w8_tables(); }
+ECGPU_API int ecgpu_galois_split_w8_multiply(int x, int y) { return split_w8_multiply(x, y); }
 
 ECGPU_API int ecgpu_galois_ilog(int value, int w) {
   int* t = ilog_table(w);

@@ -34,6 +34,7 @@
 #include <utility>
 #include <vector>
 
+#include "buffer_contract.hpp"
 #include "ecgpu.h"
 #include "gf_host.hpp"
 #include "gf_kernels.hpp"
@@ -1163,9 +1164,11 @@ int exec_staged(Ctx* c, const FusedOp& op, CallMap& m, bool inl) {
 // Runs a fused op synchronously over `size` bytes of every buffer: maps the
 // buffers, then the cheapest staging mode for the host ones (§8 of DESIGN.md;
 // the thresholds are measured, see bounce_max / zc_max / zc_out_max).
-int execute(const FusedOp& op, int64_t size) {
+int execute(const FusedOp& op, int64_t size, const char* call) {
   if (op.w != 8 && size % (op.w / 8) != 0)
     return fail(ECGPU_ERR_ARG, "w = " + std::to_string(op.w) + ": size must be a multiple of the word size");
+  // identical or disjoint buffers, checked before anything touches the GPU
+  if (int rc = check_op_buffers(call, op, size)) return rc;
   add_stats(op);
   if (op.dsts.empty() || size <= 0) return ECGPU_OK;
   const int device = current_device();
@@ -1209,6 +1212,7 @@ ECGPU_API int ecgpu_plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* 
                               int64_t size) {
   if (!p || stripes < 0 || size < 0 || (stripes && (!src_ptrs || !dst_ptrs)))
     return fail(ECGPU_ERR_ARG, "ecgpu_plan_bind: bad arguments");
+  if (int rc = ecgpu_plan_check_buffers(p->rows, p->nsrc, stripes, src_ptrs, dst_ptrs, size)) return rc;
   return plan_bind(p, stripes, src_ptrs, dst_ptrs, size, nullptr);
 }
 
@@ -1227,6 +1231,12 @@ ECGPU_API int ecgpu_plan_launch(ecgpu_plan* p, void* stream) {
 
 ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p) { plan_free(p); }
 
+ECGPU_API int ecgpu_device_pci_bus_id(int device, char* buf, int len) {
+  if (!buf || len < 13) return fail(ECGPU_ERR_ARG, "ecgpu_device_pci_bus_id: buffer of >= 13 bytes required");
+  ECGPU_HIP(hipDeviceGetPCIBusId(buf, len, device));
+  return ECGPU_OK;
+}
+
 ECGPU_API int ecgpu_host_register(void* ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return fail(ECGPU_ERR_ARG, "ecgpu_host_register: bad arguments");
   ECGPU_HIP(hipHostRegister(ptr, size_t(bytes), hipHostRegisterDefault));
@@ -1241,7 +1251,9 @@ ECGPU_API int ecgpu_host_unregister(void* ptr) {
 
 ECGPU_API int ecgpu_encode_batch(int k, int m, const int* matrix, int stripes, const uint8_t* const* data,
                                  uint8_t* const* coding, int64_t size, void* stream) {
-  if (k <= 0 || m <= 0 || !matrix) return fail(ECGPU_ERR_ARG, "ecgpu_encode_batch: bad arguments");
+  if (k <= 0 || m <= 0 || !matrix || stripes < 0 || size < 0 || (stripes && (!data || !coding)))
+    return fail(ECGPU_ERR_ARG, "ecgpu_encode_batch: bad arguments");
+  if (int rc = ecgpu_plan_check_buffers(m, k, stripes, data, coding, size)) return rc;
   ecgpu_plan* p = ecgpu_plan_create(m, k, matrix, -1);
   if (!p) return ECGPU_ERR_HIP;
   int rc = plan_bind(p, stripes, data, coding, size, static_cast<hipStream_t>(stream));
@@ -1266,7 +1278,7 @@ ECGPU_API int ecgpu_jerasure_matrix_encode(int k, int m, int w, int* matrix, cha
   if (!valid_w(w)) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_encode: w must be 8, 16 or 32");
   LinearTracker t(w);
   plan_encode(t, k, m, matrix, data_ptrs, coding_ptrs, size);
-  return execute(t.finish(), size);
+  return execute(t.finish(), size, "jerasure_matrix_encode");
 }
 
 ECGPU_API int ecgpu_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures,
@@ -1274,15 +1286,44 @@ ECGPU_API int ecgpu_jerasure_matrix_decode(int k, int m, int w, int* matrix, int
   if (!valid_w(w)) return ECGPU_ERR;  // jerasure.cpp:165: any other w returns -1
   LinearTracker t(w);
   if (plan_decode(t, k, m, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size) < 0) return ECGPU_ERR;
-  return execute(t.finish(), size);
+  return execute(t.finish(), size, "jerasure_matrix_decode");
 }
 
 ECGPU_API int ecgpu_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int dest_id,
                                             char** data_ptrs, char** coding_ptrs, int size) {
-  if (!valid_w(w)) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_dotprod: w must be 8, 16 or 32");
+  if (w == 1) {
+    // jerasure.cpp:561-620 at w = 1: coefficient 1 copies (first) or XORs the
+    // source; any other non-zero coefficient has no region multiply at w = 1
+    // (the reference's switch has no case for it) but still counts its bytes
+    // as gf and marks the destination initialised.  So the map is the XOR of
+    // the unit-coefficient sources -- the XOR-only kernel over GF(2^8)
+    // bytes, where 1 * x = x.
+    LinearTracker t(8);
+    auto buf = [&](int i) -> void* {
+      const int id = src_ids ? src_ids[i] : i;
+      return id < k ? static_cast<void*>(data_ptrs[id]) : static_cast<void*>(coding_ptrs[id - k]);
+    };
+    void* dst = dest_id < k ? static_cast<void*>(data_ptrs[dest_id]) : static_cast<void*>(coding_ptrs[dest_id - k]);
+    bool init = false;
+    for (int i = 0; i < k; ++i) {
+      if (matrix_row[i] != 1) continue;
+      if (!init) {
+        t.copy(dst, buf(i));
+        t.count(0, 0, double(size));
+        init = true;
+      } else {
+        t.xor3(buf(i), dst, dst);
+        t.count(double(size), 0, 0);
+      }
+    }
+    for (int i = 0; i < k; ++i)
+      if (matrix_row[i] != 0 && matrix_row[i] != 1) t.count(0, double(size), 0);
+    return execute(t.finish(), size, "jerasure_matrix_dotprod");
+  }
+  if (!valid_w(w)) return fail(ECGPU_ERR_ARG, "ecgpu_jerasure_matrix_dotprod: w must be 1, 8, 16 or 32");
   LinearTracker t(w);
   t.dotprod(k, matrix_row, src_ids, dest_id, data_ptrs, coding_ptrs, size);
-  return execute(t.finish(), size);
+  return execute(t.finish(), size, "jerasure_matrix_dotprod");
 }
 
 ECGPU_API int ecgpu_jerasure_do_parity(int k, char** data_ptrs, char* parity_ptr, int size) {
@@ -1290,7 +1331,7 @@ ECGPU_API int ecgpu_jerasure_do_parity(int k, char** data_ptrs, char* parity_ptr
   t.copy(parity_ptr, data_ptrs[0]);
   for (int i = 1; i < k; ++i) t.xor3(data_ptrs[i], parity_ptr, parity_ptr);
   t.count(double(size) * (k - 1), 0, double(size));
-  return execute(t.finish(), size);
+  return execute(t.finish(), size, "jerasure_do_parity");
 }
 
 ECGPU_API int ecgpu_galois_w08_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
@@ -1299,7 +1340,7 @@ ECGPU_API int ecgpu_galois_w08_region_multiply(char* region, int multby, int nby
     t.mul(region, multby, region, false);  // galois.cpp:429,447: in place, add ignored
   else
     t.mul(region, multby, r2, add != 0);
-  return execute(t.finish(), nbytes);
+  return execute(t.finish(), nbytes, "galois_w08_region_multiply");
 }
 
 // galois.cpp:469-542: nbytes/2 words; multby 0 zeroes (no add) or does
@@ -1312,20 +1353,20 @@ ECGPU_API int ecgpu_galois_w16_region_multiply(char* region, int multby, int nby
   } else {
     t.mul(region, multby, dst, r2 != nullptr && add != 0);
   }
-  return execute(t.finish(), nbytes & ~1);
+  return execute(t.finish(), nbytes & ~1, "galois_w16_region_multiply");
 }
 
 // galois.cpp:666-727: nbytes/4 words; add applies even in place.
 ECGPU_API int ecgpu_galois_w32_region_multiply(char* region, int multby, int nbytes, char* r2, int add) {
   LinearTracker t(32);
   t.mul(region, multby, r2 ? r2 : region, add != 0);
-  return execute(t.finish(), nbytes & ~3);
+  return execute(t.finish(), nbytes & ~3, "galois_w32_region_multiply");
 }
 
 ECGPU_API int ecgpu_galois_region_xor(char* r1, char* r2, char* r3, int nbytes) {
   LinearTracker t;
   t.xor3(r1, r2, r3);
-  return execute(t.finish(), nbytes);
+  return execute(t.finish(), nbytes, "galois_region_xor");
 }
 
 ECGPU_API int ecgpu_reed_sol_galois_w08_region_multby_2(char* region, int nbytes) {
@@ -1359,7 +1400,7 @@ ECGPU_API int ecgpu_reed_sol_r6_encode(int k, int w, char** data_ptrs, char** co
     t.mul(coding_ptrs[1], 2, coding_ptrs[1], false);
     t.xor3(coding_ptrs[1], data_ptrs[i], coding_ptrs[1]);
   }
-  const int rc = execute(t.finish(), size);
+  const int rc = execute(t.finish(), size, "reed_sol_r6_encode");
   return rc == ECGPU_OK ? 1 : rc;
 }
 

@@ -3,7 +3,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <mutex>
+#include <new>
 #include <vector>
 
 namespace ecgpu {
@@ -200,6 +202,45 @@ int* log_table(int w) {
 int* ilog_table(int w) {
   std::lock_guard<std::mutex> lk(g_wt_mu);
   return build_log_locked(w) < 0 ? nullptr : g_wt[w].ilog;
+}
+
+namespace {
+// split_w8[i + j][(a << 8) | b] = (a << 8i) * (b << 8j) in GF(2^32), for the
+// byte-position pairs the reference fills (i = 0: j = 0..3; i = 3: j = 1..3),
+// galois.cpp:756-789.  One allocation, built once, read-only afterwards.
+std::once_flag g_split_once;
+std::vector<int> g_split;  // 7 x 65536
+std::atomic<int> g_split_rc{-1};  // 0 once built (release), read with acquire
+}  // namespace
+
+int create_split_w8_tables() {
+  std::call_once(g_split_once, [] {
+    try {
+      g_split.assign(size_t(7) << 16, 0);
+    } catch (const std::bad_alloc&) {
+      return;  // g_split_rc stays -1, like the reference's failed malloc
+    }
+    for (int i = 0; i < 4; i += 3)
+      for (int j = i == 0 ? 0 : 1; j < 4; ++j) {
+        int* t = &g_split[size_t(i + j) << 16];
+        for (int a = 0; a < 256; ++a)
+          for (int b = 0; b < 256; ++b) t[(a << 8) | b] =
+              shift_multiply(int(uint32_t(a) << (8 * i)), int(uint32_t(b) << (8 * j)), 32);
+      }
+    g_split_rc.store(0, std::memory_order_release);
+  });
+  return g_split_rc.load(std::memory_order_acquire);
+}
+
+int split_w8_multiply(int x, int y) {
+  // galois.cpp:791-809: byte i of x times byte j of y from table i + j
+  if (g_split_rc.load(std::memory_order_acquire) != 0) return shift_multiply(x, y, 32);
+  const uint32_t ux = uint32_t(x), uy = uint32_t(y);
+  int acc = 0;
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j)
+      acc ^= g_split[(size_t(i + j) << 16) | (((ux >> (8 * i)) & 255u) << 8) | ((uy >> (8 * j)) & 255u)];
+  return acc;
 }
 
 }  // namespace ecgpu

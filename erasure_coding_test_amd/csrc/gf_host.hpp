@@ -43,5 +43,11 @@ int* log_table(int w);
 int* ilog_table(int w);  // already offset: valid index range [-(2^w-1), 2*(2^w-1))
 int create_log_tables(int w);   // 0 / -1
 int create_mult_tables(int w);  // 0 / -1
+// galois.cpp:756-809: the seven 2^16-entry byte-pair product tables of
+// GF(2^32) (built once, thread-safely; 0, or -1 if they cannot be allocated)
+// and the w = 32 multiply that reads them (computed directly while they are
+// not built, where the reference would dereference NULL).
+int create_split_w8_tables();
+int split_w8_multiply(int x, int y);
 
 }  // namespace ecgpu

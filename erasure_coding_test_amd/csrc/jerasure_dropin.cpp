@@ -37,8 +37,15 @@ namespace {
 // client_main.cpp:2118-2124); void calls print a message and exit(1), the
 // reference's convention for unrecoverable conditions (galois.cpp:330-334,
 // jerasure.cpp:291-294).
+// Buffers that break the library's contract (a written region partially
+// overlapping another region of the call, buffer_contract.hpp) take the same
+// channel: the reference's bytes for them depend on its loop order, and a
+// silently different answer would be worse than the reference's own exit.
 [[noreturn]] void gpu_fatal(const char* fn, int rc) {
-  std::fprintf(stderr, "%s: MI355X path failed (%d): %s\n", fn, rc, ecgpu_last_error());
+  if (rc == ECGPU_ERR_ARG)
+    std::fprintf(stderr, "%s: arguments rejected (%d): %s\n", fn, rc, ecgpu_last_error());
+  else
+    std::fprintf(stderr, "%s: MI355X path failed (%d): %s\n", fn, rc, ecgpu_last_error());
   std::exit(1);
 }
 
@@ -74,7 +81,7 @@ int galois_ilog(int value, int w) {
 
 int galois_create_log_tables(int w) { return ecgpu_cpu::create_log_tables(w); }
 int galois_create_mult_tables(int w) { return ecgpu_cpu::create_mult_tables(w); }
-int galois_create_split_w8_tables() { return 0; }  // w=32 multiply needs no tables here
+int galois_create_split_w8_tables() { return ecgpu_galois_create_split_w8_tables(); }
 
 int galois_logtable_multiply(int x, int y, int w) { return (x == 0 || y == 0) ? 0 : ecgpu_galois_single_multiply(x, y, w); }
 int galois_logtable_divide(int x, int y, int w) { return ecgpu_galois_single_divide(x, y, w); }
@@ -87,7 +94,7 @@ int galois_shift_divide(int a, int b, int w) {
   return ecgpu_cpu::shift_multiply(a, ecgpu_cpu::shift_inverse(b, w), w);
 }
 int galois_shift_inverse(int y, int w) { return ecgpu_cpu::shift_inverse(y, w); }
-int galois_split_w8_multiply(int x, int y) { return ecgpu_cpu::shift_multiply(x, y, 32); }
+int galois_split_w8_multiply(int x, int y) { return ecgpu_galois_split_w8_multiply(x, y); }
 
 int* galois_get_mult_table(int w) { return ecgpu_cpu::mult_table(w); }
 int* galois_get_div_table(int w) { return ecgpu_cpu::div_table(w); }
@@ -160,7 +167,8 @@ int jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int
   const int rc = ecgpu_jerasure_matrix_decode(k, m, w, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size);
   if (rc == ECGPU_ERR) return -1;
   if (rc != ECGPU_OK) {  // the reference's failure result, with the reason on stderr
-    std::fprintf(stderr, "jerasure_matrix_decode: MI355X path failed (%d): %s\n", rc, ecgpu_last_error());
+    std::fprintf(stderr, "jerasure_matrix_decode: %s (%d): %s\n",
+                 rc == ECGPU_ERR_ARG ? "arguments rejected" : "MI355X path failed", rc, ecgpu_last_error());
     return -1;
   }
   return 0;
@@ -172,7 +180,8 @@ void jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int de
     std::fprintf(stderr, "ERROR: jerasure_matrix_dotprod() called and w is not 1, 8, 16 or 32\n");
     std::exit(1);
   }
-  if (w != 1 && whole_words(w, size)) {
+  // w = 1 is byte-exact XOR / copy at any size, like w = 8
+  if (w == 1 || whole_words(w, size)) {
     check("jerasure_matrix_dotprod",
           ecgpu_jerasure_matrix_dotprod(k, w, matrix_row, src_ids, dest_id, data_ptrs, coding_ptrs, size));
     return;

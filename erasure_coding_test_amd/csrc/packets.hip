@@ -18,6 +18,7 @@
 #include <utility>
 #include <vector>
 
+#include "buffer_contract.hpp"
 #include "ecgpu.h"
 #include "gf_host.hpp"
 #include "matrix_host.hpp"
@@ -45,15 +46,12 @@ constexpr int kMaxPacketRow = (1 << 20) - 1;
 constexpr int kPacketRows = 32;  // output packet rows per launch (uint32 masks)
 
 // Slot s's packet row r of super-packet sp is ptrs[s] + sp * spstride + r * ps.
-int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride, int64_t ps) {
-  add_stats(op);
-  if (op.dsts.empty() || nsp <= 0 || ps <= 0) return ECGPU_OK;
-  const int device = current_device();
-  CtxLease lease(device);
-  if (!lease.c) return lease.rc;
-  Ctx* c = lease.c;
-  DeviceGuard g(device);
-
+int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride, int64_t ps,
+                    const char* call) {
+  if (op.dsts.empty() || nsp <= 0 || ps <= 0) {
+    add_stats(op);
+    return ECGPU_OK;
+  }
   // Slots touched and their byte extents.
   std::vector<int> slots;
   std::vector<int64_t> maxrow(ptrs.size(), -1);
@@ -72,16 +70,24 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
   for (void* k : op.dsts)
     if (int rc = touch(k, true)) return rc;
   const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
+  std::vector<int64_t> extent(ptrs.size(), 0);
+  for (int sl : slots) extent[size_t(sl)] = (nsp - 1) * spstride + (maxrow[size_t(sl)] + 1) * ps;
+  // identical or disjoint device buffers, checked before anything touches the GPU
+  if (int rc = check_slot_buffers(call, ptrs, slots, extent, is_out)) return rc;
+  add_stats(op);
+  const int device = current_device();
+  CtxLease lease(device);
+  if (!lease.c) return lease.rc;
+  Ctx* c = lease.c;
+  DeviceGuard g(device);
   const bool via_temp = op.dst_is_src && rows > kPacketRows;
   const int ngroups = (rows + kPacketRows - 1) / kPacketRows;
 
   // Staging slab: staged slots, temporaries, then the pointer / mask tables.
   std::vector<uint8_t*> base(ptrs.size(), nullptr);
   std::vector<char> staged(ptrs.size(), 0);
-  std::vector<int64_t> extent(ptrs.size(), 0);
   size_t off = 0;
   for (int sl : slots) {
-    extent[size_t(sl)] = (nsp - 1) * spstride + (maxrow[size_t(sl)] + 1) * ps;
     bool on_dev = false;
     if (int rc = classify(ptrs[size_t(sl)], device, &on_dev)) return rc;
     if (on_dev) {
@@ -269,7 +275,7 @@ ECGPU_API int ecgpu_jerasure_bitmatrix_dotprod(int k, int w, int* bitmatrix_row,
   auto put = [&](int id) { p[size_t(id)] = id < k ? data_ptrs[id] : coding_ptrs[id - k]; };
   put(dest_id);
   for (int x = 0; x < k; ++x) put(src_ids ? src_ids[x] : x);
-  return execute_packets(t.finish(), p, nsp, int64_t(w) * packetsize, packetsize);
+  return execute_packets(t.finish(), p, nsp, int64_t(w) * packetsize, packetsize, "jerasure_bitmatrix_dotprod");
 }
 
 ECGPU_API int ecgpu_jerasure_bitmatrix_encode(int k, int m, int w, int* bitmatrix, char** data_ptrs,
@@ -281,7 +287,7 @@ ECGPU_API int ecgpu_jerasure_bitmatrix_encode(int k, int m, int w, int* bitmatri
   for (int i = 0; i < m; ++i)
     record_bitmatrix_dotprod(t, k, w, bitmatrix + size_t(i) * k * w * w, nullptr, k + i, packetsize, nsp);
   return execute_packets(t.finish(), device_ptrs(k, k + m, data_ptrs, coding_ptrs), nsp, int64_t(w) * packetsize,
-                         packetsize);
+                         packetsize, "jerasure_bitmatrix_encode");
 }
 
 // jerasure.cpp:623-703 as one fused GF(2) map.
@@ -324,7 +330,7 @@ ECGPU_API int ecgpu_jerasure_bitmatrix_decode(int k, int m, int w, int* bitmatri
     if (erased[k + i]) record_bitmatrix_dotprod(t, k, w, bitmatrix + i * blk, nullptr, k + i, packetsize, nsp);
   std::free(erased);
   return execute_packets(t.finish(), device_ptrs(k, k + m, data_ptrs, coding_ptrs), nsp, int64_t(w) * packetsize,
-                         packetsize);
+                         packetsize, "jerasure_bitmatrix_decode");
 }
 
 // jerasure.cpp:1153-1176: one super-packet at ptrs.
@@ -337,7 +343,7 @@ ECGPU_API int ecgpu_jerasure_do_scheduled_operations(char** ptrs, int** operatio
   PacketTracker t(max_dev + 1, max_row + 1);
   record_schedule(t, operations, packetsize, 1);
   std::vector<char*> p(ptrs, ptrs + (max_dev + 1));
-  return execute_packets(t.finish(), p, 1, 0, packetsize);
+  return execute_packets(t.finish(), p, 1, 0, packetsize, "jerasure_do_scheduled_operations");
 }
 
 // jerasure.cpp:1178-1192 over nptrs device pointers (NULL where unused), and
@@ -353,7 +359,7 @@ ECGPU_API int ecgpu_schedule_run(int nptrs, char** ptrs, int** operations, int w
   PacketTracker t(max_dev + 1, max_row + 1);
   record_schedule(t, operations, packetsize, nsp);
   std::vector<char*> p(ptrs, ptrs + nptrs);
-  return execute_packets(t.finish(), p, nsp, int64_t(w) * packetsize, packetsize);
+  return execute_packets(t.finish(), p, nsp, int64_t(w) * packetsize, packetsize, "jerasure_schedule");
 }
 
 ECGPU_API int ecgpu_jerasure_schedule_encode(int k, int m, int w, int** schedule, char** data_ptrs, char** coding_ptrs,

@@ -19,6 +19,7 @@
 #include <utility>
 #include <vector>
 
+#include "buffer_contract.hpp"
 #include "ecgpu.h"
 #include "gf_host.hpp"
 #include "host_sync.hpp"
@@ -220,6 +221,11 @@ ECGPU_API ecgpu_pipeline* ecgpu_pipeline_create_decode(int k, int m, int w, cons
 // worker when an output is pageable or an earlier D2H is still unissued.
 ECGPU_API int64_t ecgpu_pipeline_submit(ecgpu_pipeline* p, char** data_ptrs, char** coding_ptrs) {
   if (!p || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_submit: bad arguments");
+  // an output sharing bytes with another shard of the stripe: rejected before
+  // anything is queued (buffer_contract.hpp)
+  if (int rc = check_stripe_buffers("ecgpu_pipeline_submit", p->dev.k, data_ptrs, coding_ptrs, p->dev.src_ids,
+                                    p->dev.out_ids, p->dev.size))
+    return rc;
   DeviceGuard g(p->dev.device);
   return p->core->submit(data_ptrs, coding_ptrs);
 }
@@ -338,6 +344,12 @@ ECGPU_API ecgpu_pipeline_group* ecgpu_pipeline_group_create_decode(int k, int m,
 
 ECGPU_API int64_t ecgpu_pipeline_group_submit(ecgpu_pipeline_group* g, char** data_ptrs, char** coding_ptrs) {
   if (!g || !data_ptrs || !coding_ptrs) return fail(ECGPU_ERR_ARG, "ecgpu_pipeline_group_submit: bad arguments");
+  // checked here, before a ticket is taken, so a rejected stripe leaves no gap
+  // in the member queues (every member runs the same shard map)
+  const PipeDevice& d0 = g->members[0]->p->dev;
+  if (int rc = check_stripe_buffers("ecgpu_pipeline_group_submit", d0.k, data_ptrs, coding_ptrs, d0.src_ids,
+                                    d0.out_ids, d0.size))
+    return rc;
   const int64_t n = int64_t(g->members.size());
   const int64_t t = g->next_ticket.fetch_add(1);
   GroupMember& mb = *g->members[size_t(t % n)];

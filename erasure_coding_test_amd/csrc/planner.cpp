@@ -131,6 +131,8 @@ FusedOp LinearTracker::finish() const {
     op.dsts.push_back(bufs_[outs[r]]);
     if (col[outs[r]] >= 0) op.dst_is_src = true;
   }
+  op.touched = bufs_;
+  op.touched_written = written_;
   op.w = w_;
   op.xor_bytes = xor_;
   op.gf_bytes = gf_;

@@ -26,6 +26,11 @@ struct FusedOp {
   // Reference byte counters (jerasure.cpp:42-44): xor, gf-multiply, memcpy.
   double xor_bytes = 0, gf_bytes = 0, memcpy_bytes = 0;
   bool dst_is_src = false;     // some output buffer is also read
+  // Every buffer the replayed sequence named (first-use order) and whether the
+  // sequence wrote it -- what the buffer contract is checked on
+  // (buffer_contract.hpp), including buffers whose terms cancel out of the map.
+  std::vector<void*> touched;
+  std::vector<char> touched_written;
 };
 
 class LinearTracker {

@@ -143,6 +143,8 @@ void add_stats(const FusedOp& op);
 bool inline_ok(const FusedOp& op, int64_t size);
 int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, const std::vector<uint8_t*>& dp,
                   int64_t size, hipStream_t s, bool host_io);
-int execute(const FusedOp& op, int64_t size);
+// Runs a fused op synchronously; `call` names the entry point in errors
+// (e.g. a buffer-contract rejection, buffer_contract.hpp).
+int execute(const FusedOp& op, int64_t size, const char* call = "ecgpu");
 
 ECGPU_RT_END

@@ -20,7 +20,7 @@ void region_multiply_w16(char* region, int multby, int nbytes, char* r2, int add
 void region_multiply_w32(char* region, int multby, int nbytes, char* r2, int add);
 void region_xor(const char* r1, const char* r2, char* r3, long nbytes);
 
-// jerasure.cpp:561-620 for w in {1, 16, 32}; :153-254 for w in {16, 32}.
+// jerasure.cpp:561-620 for w in {16, 32} (ragged sizes); :153-254 for w in {16, 32}.
 void matrix_dotprod(int k, int w, const int* row, const int* src_ids, int dest_id, char** data, char** coding,
                     int size);
 int matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data, char** coding,

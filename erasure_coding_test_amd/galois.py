@@ -58,8 +58,9 @@ def galois_create_mult_tables(w: int) -> int:
 
 
 def galois_create_split_w8_tables() -> int:
-    """0: the w = 32 multiply here needs no split tables (galois.cpp:756-789)."""
-    return 0
+    """Builds the seven byte-pair product tables of GF(2^32) once: 0, or -1 if
+    they cannot be allocated (galois.cpp:756-789)."""
+    return N.lib.ecgpu_galois_create_split_w8_tables()
 
 
 def galois_logtable_multiply(x: int, y: int, w: int) -> int:
@@ -102,8 +103,10 @@ def galois_shift_divide(a: int, b: int, w: int) -> int:
 
 
 def galois_split_w8_multiply(x: int, y: int) -> int:
-    """The w = 32 product the reference assembles from 8-bit split tables (galois.cpp:791-810)."""
-    return N.lib.ecgpu_galois_shift_multiply(x, y, 32)
+    """The w = 32 product assembled from the 8-bit split tables (galois.cpp:791-810;
+    computed directly before galois_create_split_w8_tables, where the reference
+    would dereference NULL)."""
+    return N.lib.ecgpu_galois_split_w8_multiply(x, y)
 
 
 def _table(ptr, n: int, offset: int = 0):

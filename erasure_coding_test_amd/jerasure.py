@@ -45,8 +45,8 @@ def jerasure_matrix_decode(k: int, m: int, w: int, matrix, row_k_ones: int, eras
 
 def jerasure_matrix_dotprod(k: int, w: int, matrix_row, src_ids: Optional[Sequence[int]], dest_id: int, data_ptrs,
                             coding_ptrs, size: int) -> None:
-    if w not in (8, 16, 32):
-        raise ValueError("jerasure_matrix_dotprod: w must be 8, 16 or 32")
+    if w not in (1, 8, 16, 32):  # jerasure.cpp:569-572
+        raise ValueError("jerasure_matrix_dotprod: w must be 1, 8, 16 or 32")
     ids = None if src_ids is None else N.int_array(src_ids)
     rc = N.lib.ecgpu_jerasure_matrix_dotprod(k, w, N.int_array(matrix_row), ids, dest_id,
                                              N.ptr_array(addrs(data_ptrs)), N.ptr_array(addrs(coding_ptrs)), size)

@@ -20,7 +20,10 @@
  * (classified per buffer; host buffers are staged through HBM) and are
  * synchronous: results are valid on return, like the reference.  They never
  * fall back to a CPU path; a HIP failure returns ECGPU_ERR_HIP (or, through
- * the void-returning drop-in names, aborts with a message).
+ * the void-returning drop-in names, exits with a message).  Buffers of one
+ * call are identical or disjoint: a written region that partially overlaps
+ * another region of the call returns ECGPU_ERR_ARG before anything runs
+ * (see ecgpu_plan_check_buffers).
  *
  * Host-only (no GPU touched): field arithmetic, matrix construction,
  * inversion and decode planning.
@@ -81,6 +84,10 @@ ECGPU_API int* ecgpu_galois_get_log_table(int w);
 ECGPU_API int* ecgpu_galois_get_ilog_table(int w);
 ECGPU_API int ecgpu_galois_shift_multiply(int a, int b, int w);  /* galois.cpp:292-320 */
 ECGPU_API int ecgpu_galois_shift_inverse(int a, int w);          /* galois.cpp:605-625 */
+/* The w = 32 split tables: 0 (or -1 if they cannot be allocated), and the
+ * product read from them (galois.cpp:756-789, :791-809). */
+ECGPU_API int ecgpu_galois_create_split_w8_tables(void);
+ECGPU_API int ecgpu_galois_split_w8_multiply(int x, int y);
 
 /* ------------------------------------------- matrices (host only) ------- */
 ECGPU_API int* ecgpu_reed_sol_vandermonde_coding_matrix(int k, int m, int w);            /* reed_sol.cpp:63-84   */
@@ -115,7 +122,8 @@ ECGPU_API int ecgpu_jerasure_matrix_encode(int k, int m, int w, int* matrix, cha
 /* jerasure.cpp:153-254.  Returns 0 / -1 like the reference. */
 ECGPU_API int ecgpu_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures,
                                            char** data_ptrs, char** coding_ptrs, int size);
-/* jerasure.cpp:561-620 */
+/* jerasure.cpp:561-620.  w = 1, 8, 16 or 32 (w = 1: the XOR of the sources
+ * whose coefficient is 1, as in the reference, which has no w = 1 multiply). */
 ECGPU_API int ecgpu_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int dest_id,
                                             char** data_ptrs, char** coding_ptrs, int size);
 /* jerasure.cpp:347-358 */
@@ -180,6 +188,17 @@ typedef struct ecgpu_plan ecgpu_plan;
 ECGPU_API ecgpu_plan* ecgpu_plan_create(int rows, int nsrc, const int* coefs, int device);
 ECGPU_API int ecgpu_plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src_ptrs, uint8_t* const* dst_ptrs,
                               int64_t size);
+/* The buffer contract of a bind (host only; ecgpu_plan_bind and
+ * ecgpu_encode_batch run it first): ECGPU_ERR_ARG, naming the pair in
+ * ecgpu_last_error(), when an output shares a byte with another buffer of the
+ * bind -- except an output identical to a source of its own stripe with
+ * rows <= 4 (one launch; each column is read before it is written).  The
+ * synchronous calls above apply the same rule (identical or disjoint):
+ * identical pointers follow the reference's sequential semantics, partially
+ * overlapping regions that are written are rejected, because the reference's
+ * bytes for them depend on its loop order (galois.cpp:452-465, :731-754). */
+ECGPU_API int ecgpu_plan_check_buffers(int rows, int nsrc, int stripes, const uint8_t* const* src_ptrs,
+                                       uint8_t* const* dst_ptrs, int64_t size);
 /* kind: ECGPU_KERNEL_PERM (production) or ECGPU_KERNEL_LDS; nontemporal: store
  * cache policy of the production kernel: 0 plain, 1 non-temporal (the
  * default; larger values clamp to 1); its loads are always non-temporal. */
@@ -250,6 +269,9 @@ ECGPU_API int ecgpu_pipeline_group_wait(ecgpu_pipeline_group* g, int64_t ticket)
 ECGPU_API int ecgpu_pipeline_group_drain(ecgpu_pipeline_group* g);
 ECGPU_API int ecgpu_pipeline_group_size(ecgpu_pipeline_group* g);
 ECGPU_API void ecgpu_pipeline_group_destroy(ecgpu_pipeline_group* g);
+/* The PCI bus id ("domain:bus:device.function") of a device
+ * (hipDeviceGetPCIBusId): which physical GPU a rank ran on (bench.py). */
+ECGPU_API int ecgpu_device_pci_bus_id(int device, char* buf, int len);
 /* Page-lock caller memory for asynchronous DMA (hipHostRegister). */
 ECGPU_API int ecgpu_host_register(void* ptr, int64_t bytes);
 ECGPU_API int ecgpu_host_unregister(void* ptr);

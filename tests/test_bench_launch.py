@@ -88,3 +88,47 @@ def test_world_size_mismatch_exits_nonzero():
                        text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode == 2
     assert "WORLD_SIZE=3" in r.stderr
+
+
+def test_distinct_devices_check():
+    two = [{"rank": 0, "pci_bus_id": "0000:05:00.0"}, {"rank": 1, "pci_bus_id": "0000:05:00.0"}]
+    ok, note = bench.distinct_devices(two, rehearsal=False)
+    assert not ok and "ranks [0, 1] on 0000:05:00.0" in note
+    assert bench.distinct_devices(two, rehearsal=True)[0]  # a labelled rehearsal shares cuda:0 on purpose
+    two[1]["pci_bus_id"] = "0000:15:00.0"
+    assert bench.distinct_devices(two, rehearsal=False) == (True, "2 ranks on 2 distinct GPUs (PCI bus ids)")
+    two[1]["pci_bus_id"] = None
+    two[1]["uuid"] = None
+    assert not bench.distinct_devices(two, rehearsal=False)[0]  # unproven is a failure
+    assert bench.distinct_devices(two[:1], rehearsal=False)[0]
+
+
+def test_selftest_fails_ranks_on_one_device():
+    """End to end through spawn -> gloo -> gather: two ranks claiming the same
+    device make rank 0 exit non-zero, with the reason in the line."""
+    env = _env()
+    env["ECGPU_SELFTEST_SAME_BUS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--spawn-selftest"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 1, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    assert d["distinct_devices_ok"] is False and "share a GPU" in r.stderr
+    env["ECGPU_BENCH_ONE_DEVICE"] = "1"  # the rehearsal flag suppresses the check
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--spawn-selftest"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_cgroup_cpu_quota(tmp_path):
+    assert bench.cgroup_cpu_quota(str(tmp_path)) is None  # no cgroup files: unlimited
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert bench.cgroup_cpu_quota(str(tmp_path)) is None
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")
+    assert bench.cgroup_cpu_quota(str(tmp_path)) == 16
+    (tmp_path / "cpu.max").unlink()
+    (tmp_path / "cpu").mkdir()
+    (tmp_path / "cpu" / "cpu.cfs_quota_us").write_text("800000\n")
+    (tmp_path / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert bench.cgroup_cpu_quota(str(tmp_path)) == 8
+    assert 1 <= len(bench.host_cpus()) <= bench.HOST_THREAD_CAP
+    assert len(bench.all_host_cpus()) >= len(bench.host_cpus())

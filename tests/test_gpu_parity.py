@@ -899,8 +899,7 @@ def test_wide_word_matrix_coding_device(ec, gpu, w, size, offset):
     """w = 16 / 32 encode + decode on device tensors (16-B column kernel,
     word-tail kernel, misaligned base) against the reference library."""
     import torch
-    if size % (w // 8):
-        pytest.skip("not whole words")
+    assert size % (w // 8) == 0  # whole words: ragged sizes are the CPU surface's (test_surface_cpu.py)
     ref = _ref_nsa()
     k, m = 6, 3
     M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w)
@@ -1007,10 +1006,14 @@ _PIPE_SHAPES = [(1, 1), (2, 2), (3, 4), (4, 1), (5, 3), (6, 4), (7, 2), (8, 3), 
                 (13, 3), (14, 2), (15, 3), (16, 4), (10, 6)]
 
 
+# every shape at 3 column blocks; the column loop run many times (1600
+# blocks) on three shapes -- explicit lists, so no test ID exists only to skip
+_PIPE_CASES = [(k, m, 3) for k, m in _PIPE_SHAPES] + [(k, m, 1600) for k, m in ((10, 4), (16, 4), (5, 3))]
+
+
 @pytest.mark.parametrize("w", [16, 32])
 @pytest.mark.parametrize("structure", ["vandermonde", "random"])
-@pytest.mark.parametrize("k,m", _PIPE_SHAPES)
-@pytest.mark.parametrize("blocks", [3, 1600])
+@pytest.mark.parametrize("k,m,blocks", _PIPE_CASES)
 @pytest.mark.parametrize("pipe", ["2", "1"])
 def test_wide_word_pipelined_launches(ec, gpu, monkeypatch, w, structure, k, m, blocks, pipe):
     """Launches of whole 256-column blocks (4 KiB per shard each) run
@@ -1022,8 +1025,6 @@ def test_wide_word_pipelined_launches(ec, gpu, monkeypatch, w, structure, k, m, 
     one resident round).  Encode and a decode of up to m erasures against the
     reference library."""
     import torch
-    if blocks > 3 and (k, m) not in [(10, 4), (16, 4), (5, 3)]:
-        pytest.skip("large sizes on three shapes")
     monkeypatch.delenv("ECGPU_WIDE", raising=False)
     monkeypatch.delenv("ECGPU_NIB16", raising=False)
     monkeypatch.delenv("ECGPU_WIDE_UNITS", raising=False)

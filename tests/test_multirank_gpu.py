@@ -176,6 +176,13 @@ def test_bench_gpus2_rehearsal_spawns_two_ranks(gpu):
     e2e = d["e2e"]
     assert e2e["encode"]["parity_ok"] and e2e["encode"]["data_GiBps"] > 1
     assert e2e["decode"]["rebuilt_ok"] and e2e["decode"]["erasures"] == [0]
+    assert d["e2e_ok"] is True
+    # each rank names its physical GPU; both sit on cuda:0 here, which the
+    # rehearsal flag exempts from the distinct-device check
+    buses = [p["pci_bus_id"] for p in d["per_rank"]]
+    assert all(b and b.count(":") == 2 for b in buses) and buses[0] == buses[1], buses
+    assert d["distinct_devices_ok"] is True and "rehearsal" in d["distinct_devices"]
+    assert d["cpu_baseline_per_gpu_share"]["cores"] >= 1 and d["cpu_baseline_all_cores"]["cores"] >= 1
 
 
 def test_bench_gpus_beyond_visible_devices_fails(gpu):

@@ -40,6 +40,9 @@ SIGNATURES = {
     "ecgpu_version": (c_char_p, []),
     "ecgpu_build_id": (c_char_p, [c_int]),
     "ecgpu_last_error": (c_char_p, []),
+    "ecgpu_set_knob": (c_int, [c_char_p, c_int]),
+    "ecgpu_reset_knob": (c_int, [c_char_p]),
+    "ecgpu_get_knob": (c_int, [c_char_p, c_int_p]),
     "ecgpu_free": (None, [c_void_p]),
     "ecgpu_galois_single_multiply": (c_int, [c_int, c_int, c_int]),
     "ecgpu_galois_single_divide": (c_int, [c_int, c_int, c_int]),
@@ -140,6 +143,22 @@ for _name, (_res, _args) in SIGNATURES.items():
 
 class EcgpuError(RuntimeError):
     pass
+
+
+def set_knob(name: str, value: int) -> None:
+    """Override a tuning knob for this process (ecgpu_set_knob; knobs.hpp)."""
+    check(lib.ecgpu_set_knob(name.encode(), int(value)), "ecgpu_set_knob")
+
+
+def reset_knob(name=None) -> None:
+    """Back to the environment's value (None: every knob)."""
+    check(lib.ecgpu_reset_knob(None if name is None else name.encode()), "ecgpu_reset_knob")
+
+
+def get_knob(name: str) -> int:
+    v = c_int()
+    check(lib.ecgpu_get_knob(name.encode(), ctypes.byref(v)), "ecgpu_get_knob")
+    return v.value
 
 
 def last_error() -> str:

@@ -41,12 +41,12 @@ ARCH = os.environ.get("ECGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 
-HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp", "contract_host.cpp"]
+HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp", "contract_host.cpp", "knobs.cpp"]
 # (source, object, extra flags): the specialised kernel table is split into
 # one translation unit per output-row count so the four compile in parallel
 HIP_UNITS = [(f, f + ".o", []) for f in ("ecgpu_runtime.hip", "accum.hip", "pipeline.hip", "packets.hip")] + [
     ("gf_spec.hip", f"gf_spec_r{r}.hip.o", [f"-DECGPU_SPEC_R={r}"]) for r in (1, 2, 3, 4)]
-HDRS = ["buffer_contract.hpp", "gf_host.hpp", "host_sync.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp", "gf_spec.hpp",
+HDRS = ["buffer_contract.hpp", "gf_host.hpp", "knobs.hpp", "host_sync.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp", "gf_spec.hpp",
         "runtime.hpp"]
 DROPIN_SRCS = ["jerasure_dropin.cpp", "jerasure_surface.cpp"]
 
@@ -72,7 +72,7 @@ def _run_parallel(cmds):
 
 
 KERNEL_ID_SRCS = ["gf_kernels.hpp", "gf_spec.hip", "gf_spec.hpp", "ecgpu_runtime.hip", "runtime.hpp", "planner.cpp",
-                  "planner.hpp"]
+                  "planner.hpp", "knobs.cpp", "knobs.hpp"]
 
 
 def _digest(parts, files) -> str:

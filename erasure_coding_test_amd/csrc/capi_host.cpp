@@ -5,6 +5,7 @@
 
 #include "ecgpu.h"
 #include "gf_host.hpp"
+#include "knobs.hpp"
 #include "matrix_host.hpp"
 #include "planner.hpp"
 #include "schedule_host.hpp"
@@ -57,13 +58,10 @@ constexpr int64_t kDefaultSkew = 10 << 10;
 ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size) {
   if (size < 0) size = 0;
   const int64_t rounded = (size + 255) & ~int64_t(255);
-  // ECGPU_SHARD_SKEW_KIB: one skew for every size (A/B runs of whole
-  // workloads; read per call, like ECGPU_INLINE)
-  if (const char* e = std::getenv("ECGPU_SHARD_SKEW_KIB")) {
-    char* end = nullptr;
-    const long v = std::strtol(e, &end, 10);
-    if (end != e && *end == '\0' && v >= 0 && v <= 1024) return rounded + int64_t(v) * 1024;
-  }
+  // the shard_skew_kib knob (ECGPU_SHARD_SKEW_KIB): one skew for every size
+  // (A/B runs of whole workloads); outside 0..1024 the table applies
+  const int v = knob(Knob::kShardSkewKib);
+  if (v >= 0 && v <= 1024) return rounded + int64_t(v) * 1024;
   int64_t skew = kDefaultSkew;
   for (const SkewClass& c : kSkewTable)
     if (rounded >= c.size - c.size / 16 && rounded <= c.size + c.size / 16) skew = c.skew;

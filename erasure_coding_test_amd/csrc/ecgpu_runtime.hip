@@ -40,6 +40,7 @@
 #include "gf_kernels.hpp"
 #include "gf_spec.hpp"
 #include "host_sync.hpp"
+#include "knobs.hpp"
 #include "matrix_host.hpp"
 #include "planner.hpp"
 #include "runtime.hpp"
@@ -58,11 +59,6 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
-
-int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return (v && *v) ? std::atoi(v) : dflt;
-}
 
 // ------------------------------------------------------- kernel tables ----
 using KernelFn = void (*)(ApplyArgs);
@@ -116,12 +112,11 @@ hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t 
 unsigned residency_lds_bytes(int device, int streams) {
   static std::once_flag once;
   static int per_cu = 0;
-  static int fixed = -1;
   std::call_once(once, [&] {
     if (hipDeviceGetAttribute(&per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess)
       per_cu = 0;
-    fixed = env_int("ECGPU_BLOCKS_PER_CU", -1);
   });
+  const int fixed = knob(Knob::kBlocksPerCu);
   const int blocks = fixed >= 0 ? fixed : (streams <= 9 ? 4 : 3);
   if (blocks <= 0 || per_cu <= 0) return 0;
   const unsigned b = unsigned(per_cu / blocks) & ~511u;
@@ -136,10 +131,10 @@ unsigned residency_lds_bytes(int device, int streams) {
 //     2.5 non-unit coefficients per shard touched): decode{0} +9 %, RS(6,3)
 //     +6 %; the 40-multiply decode{0,1,2,3} needs the occupancy (-7 % capped).
 // The store policy is the plan's `nt` field (0 plain, 1 nt -- the default;
-// ECGPU_NT, ecgpu_plan_set_kernel); ECGPU_CAP (0 = never,
+// ECGPU_NT, ecgpu_plan_set_kernel); the cap knob (ECGPU_CAP: 0 = never,
 // 1 = always) overrides the cap rule.
 bool cap_for(int K, int R, int mul_terms) {
-  static const int v = env_int("ECGPU_CAP", -1);
+  const int v = knob(Knob::kCap);
   return v < 0 ? 2 * mul_terms <= 5 * (K + R) : (v != 0);
 }
 
@@ -294,8 +289,8 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
   p->rows = rows;
   p->nsrc = nsrc;
   p->w = w;
-  p->kind = env_int("ECGPU_KERNEL", ECGPU_KERNEL_PERM);
-  p->nt = std::min(kStorePolicies - 1, std::max(0, env_int("ECGPU_NT", 1)));
+  p->kind = knob(Knob::kKernel);
+  p->nt = std::min(kStorePolicies - 1, std::max(0, knob(Knob::kNt)));
   const size_t n = size_t(rows) * nsrc;
   p->coef.resize(n);
   if (w != 8) {
@@ -426,14 +421,14 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
   const int64_t byte0 = nvec * 16;
   const dim3 block(dev::kBlock);
   constexpr int kMaxGridY = 65535;
-  const bool force_perm = env_int("ECGPU_WIDE", 0) == 1;
+  const bool force_perm = knob(Knob::kWidePerm) == 1;
   for (int r0 = 0; r0 < p->rows; r0 += dev::kMaxRows) {
     const int R = std::min(dev::kMaxRows, p->rows - r0);
     // w = 16 packs two rows per LDS dword (gf_apply_wide_nib16, half the LDS bytes)
-    const bool pack16 = W == 2 && env_int("ECGPU_NIB16", 1) != 0;
+    const bool pack16 = W == 2 && knob(Knob::kNib16) != 0;
     // the 32-bit-entry kernel's unit structure (gf_apply_wide_nib<R, 1>): the
     // launch's row 0 and column 0 all ones, as in every Vandermonde encode
-    bool unit_rc = !pack16 && R >= 2 && env_int("ECGPU_WIDE_UNITS", 1) != 0;
+    bool unit_rc = !pack16 && R >= 2 && knob(Knob::kWideUnits) != 0;
     for (int j = 0; j < K && unit_rc; ++j) unit_rc = p->coef[size_t(r0) * K + j] == 1u;
     for (int r = 0; r < R && unit_rc; ++r) unit_rc = p->coef[size_t(r0 + r) * K] == 1u;
     const unsigned nib_lds = pack16 ? unsigned(K) * unsigned(dev::nib16_source_bytes(R))
@@ -477,7 +472,7 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
     // K = 10 -- profiles/r03_wide_lab.jsonl, "r03 pipe K sweep").
     // ECGPU_WIDE_PIPE: 1 that rule (default), 0 never, 2 every whole-block
     // launch of every mode (tests, A/B).
-    const int pipe = env_int("ECGPU_WIDE_PIPE", 1);
+    const int pipe = knob(Knob::kWidePipe);
     const bool pipe_shape = pipe == 2 || (pipe == 1 && !pack16 && unit_rc && K >= 7 && K <= 10);
     if (nib && nvec > 0 && nvec % dev::kBlock == 0 && pipe_shape)
       if (KernelFn f = wide_pipe_kernel(K, R, pack16 ? dev::kPipeW16 : unit_rc ? dev::kPipeW32Unit : dev::kPipeW32))
@@ -514,7 +509,7 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
           // ECGPU_WIDE16_BPCU overrides (0: the occupancy).
           int bpcu = resident_blocks(vec_fn, nib_lds);
           if (pack16) {
-            const int cap16 = env_int("ECGPU_WIDE16_BPCU", 3);
+            const int cap16 = knob(Knob::kWide16Bpcu);
             if (cap16 > 0) bpcu = std::min(bpcu, cap16);
           }
           const int64_t per_stripe = std::max<int64_t>(1, int64_t(multiprocessors(p->device)) * bpcu / ns);
@@ -608,7 +603,7 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
 hostsync::IdlePool<Ctx> g_pool;  // idle contexts (process lifetime)
 
 int current_device() {
-  const int forced = env_int("ECGPU_DEVICE", -1);
+  const int forced = knob(Knob::kDevice);
   if (forced >= 0) return forced;
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess) d = 0;
@@ -681,17 +676,9 @@ int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int 
 //     (copy_shards).  Staging large calls through a pinned ring filled by
 //     this thread instead lost 10-40 % (a single thread copies cold memory at
 //     ~35 GB/s, below the link; profiles/r02_dropin_ab.txt).
-constexpr size_t kBounceMax = size_t(2) << 20;
+size_t bounce_max() { return size_t(std::max(0, knob(Knob::kBounceKib))) << 10; }  // 2 MiB by default
 
-size_t bounce_max() {
-  static const size_t v = size_t(env_int("ECGPU_BOUNCE_KIB", int(kBounceMax >> 10))) << 10;
-  return v;
-}
-
-size_t zc_max() {
-  static const size_t v = size_t(env_int("ECGPU_ZC_KIB", 1024)) << 10;
-  return v;
-}
+size_t zc_max() { return size_t(std::max(0, knob(Knob::kZcKib))) << 10; }
 
 // A call above bounce_max() whose staged outputs total at most zc_out_max()
 // bytes, each at most zc_out_shard_max(), has the kernel write its outputs
@@ -699,22 +686,13 @@ size_t zc_max() {
 // 1 MiB shard but runs at link rate from 4 MiB (86 us): drop-in C2 encode 333
 // -> 296 us, C3 decode{0} (one 4 MiB output) 871 -> 1005 us if it took this
 // path (profiles/r02_zc_out_ab.txt).
-size_t zc_out_max() {
-  static const size_t v = size_t(env_int("ECGPU_ZC_OUT_KIB", 4096)) << 10;
-  return v;
-}
+size_t zc_out_max() { return size_t(std::max(0, knob(Knob::kZcOutKib))) << 10; }
 
-size_t zc_out_shard_max() {
-  static const size_t v = size_t(env_int("ECGPU_ZC_OUT_SHARD_KIB", 1024)) << 10;
-  return v;
-}
+size_t zc_out_shard_max() { return size_t(std::max(0, knob(Knob::kZcOutShardKib))) << 10; }
 
-bool zero_copy_pinned() {
-  static const bool v = env_int("ECGPU_ZC_PINNED", 1) != 0;
-  return v;
-}
+bool zero_copy_pinned() { return knob(Knob::kZcPinned) != 0; }
 
-bool inline_enabled() { return env_int("ECGPU_INLINE", 1) != 0; }  // per call (A/B in one process)
+bool inline_enabled() { return knob(Knob::kInline) != 0; }
 
 int ensure_bounce(Ctx* c, size_t bytes) {
   if (bytes <= c->bounce_cap) return ECGPU_OK;
@@ -825,7 +803,7 @@ void add_stats(const FusedOp& op) {
 // shard.  ECGPU_PIPE_2D=0 always copies per shard.  Used by the pipelines and
 // by synchronous calls on large host buffers.
 int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>& hp, size_t bytes, hipStream_t s) {
-  static const bool two_d = env_int("ECGPU_PIPE_2D", 1) != 0;
+  const bool two_d = knob(Knob::kPipe2d) != 0;
   const size_t n = hp.size();
   for (size_t a = 0; a < n;) {
     size_t b = a + 1;  // [a, b): maximal run with one pitch >= bytes
@@ -890,7 +868,7 @@ bool inline_ok(const FusedOp& op, int64_t size) {
   // a plan needs would cost more than the spills.
   const bool spills = nsrc >= 15 && rows >= dev::kMaxRows && size > (int64_t(1) << 20);
   return inline_enabled() && op.w == 8 && nsrc >= 1 && nsrc <= dev::kMaxSpecK && rows >= 1 && !spills &&
-         env_int("ECGPU_KERNEL", ECGPU_KERNEL_PERM) == ECGPU_KERNEL_PERM && !(op.dst_is_src && rows > dev::kMaxRows);
+         knob(Knob::kKernel) == ECGPU_KERNEL_PERM && !(op.dst_is_src && rows > dev::kMaxRows);
 }
 
 // Workgroups of an inline launch that reads or writes host memory in place
@@ -899,10 +877,7 @@ bool inline_ok(const FusedOp& op, int64_t size) {
 // flight; tools/zero_copy_probe.cpp); through the drop-in, 32-64 workgroups
 // were best (C3 pinned encode 0.83 ms vs 0.93-0.96 uncapped,
 // profiles/r02_zc_grid_sweep.txt).  0 = uncapped.
-int64_t zc_grid() {
-  static const int64_t v = env_int("ECGPU_ZC_GRID", 64);
-  return v;
-}
+int64_t zc_grid() { return knob(Knob::kZcGrid); }
 
 // One gf_apply_inl launch per <= 4 output rows over `size` bytes.  host_io:
 // some pointer is host memory the kernel reads / writes over PCIe (grid

@@ -142,7 +142,7 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
   // lanes, 2 the unpipelined 16-B kernel (A/B, RS(10,4) w = 8 64 MiB
   // bit-matrix encode on MI355X: pipelined 16-B lanes 180.5 us, unpipelined
   // with 8 rows in flight 187, 8-B lanes 190; profiles/r02_packet_ab.txt)
-  const int packet_kind = env_int("ECGPU_PACKET", 0);
+  const int packet_kind = knob(Knob::kPacket);
   bool wide16 = aligned && packet_kind != 1 && ps % 16 == 0 && spstride % 16 == 0 && dstride % 16 == 0;
   for (auto* p : sb) wide16 &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
   for (auto* p : db) wide16 &= (reinterpret_cast<uintptr_t>(p) & 15u) == 0;

@@ -103,10 +103,7 @@ struct PipeDevice {
   std::string last_error() const { return t_err; }
 };
 
-bool pipe_d2h_worker_enabled() {
-  static const bool v = env_int("ECGPU_PIPE_D2H_WORKER", 1) != 0;
-  return v;
-}
+bool pipe_d2h_worker_enabled() { return knob(Knob::kPipeD2hWorker) != 0; }
 }  // namespace
 
 extern "C" {
@@ -178,11 +175,11 @@ ecgpu_pipeline* pipeline_build(int k, int m, int rows, int nsrc, const int* coef
       d.plans.push_back(pl);
     }
   }
-  // ECGPU_TEST_D2H_DELAY_US (tests only): the D2H worker sleeps between
-  // taking a job and issuing it, which widens the window in which the
-  // submitting thread races it
+  // the test_d2h_delay_us knob (tests only, no environment variable: set with
+  // ecgpu_set_knob): the D2H worker sleeps between taking a job and issuing
+  // it, which widens the window in which the submitting thread races it
   p->core = std::make_unique<hostsync::StripePipeline<PipeDevice>>(
-      &p->dev, depth, pipe_d2h_worker_enabled(), std::max(0, env_int("ECGPU_TEST_D2H_DELAY_US", 0)));
+      &p->dev, depth, pipe_d2h_worker_enabled(), std::max(0, knob(Knob::kTestD2hDelayUs)));
   return p;
 }
 }  // namespace

@@ -19,6 +19,7 @@
 
 #include "ecgpu.h"
 #include "gf_kernels.hpp"
+#include "knobs.hpp"
 #include "planner.hpp"
 
 #define ECGPU_RT_BEGIN \
@@ -61,8 +62,7 @@ ECGPU_RT_BEGIN
 
 // ---- errors and knobs -------------------------------------------------------
 extern thread_local std::string t_err;  // ecgpu_last_error()
-int fail(int code, const std::string& msg);
-int env_int(const char* name, int dflt);
+int fail(int code, const std::string& msg);  // knobs: knobs.hpp
 
 #define ECGPU_HIP(expr)                                                                          \
   do {                                                                                           \

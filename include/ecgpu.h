@@ -61,6 +61,15 @@ ECGPU_API const char* ecgpu_version(void);
  * PMC record of a launch is valid for). */
 ECGPU_API const char* ecgpu_build_id(int what);
 ECGPU_API const char* ecgpu_last_error(void);         /* thread-local message */
+/* Tuning / A-B switches (knobs.hpp lists them: the residency cap, engines,
+ * store policy, wide-word forms, staging thresholds, shard skew).  Each is
+ * read once from its ECGPU_* environment variable at first use; set_knob
+ * overrides it for the whole process (name = "ECGPU_CAP" or "cap"), reset_knob
+ * restores the environment's value (NULL: every knob).  ECGPU_ERR_ARG for an
+ * unknown name.  Plans take the engine / store-policy knobs when created. */
+ECGPU_API int ecgpu_set_knob(const char* name, int value);
+ECGPU_API int ecgpu_reset_knob(const char* name);
+ECGPU_API int ecgpu_get_knob(const char* name, int* value);
 ECGPU_API void ecgpu_free(void* p);                    /* == free()           */
 
 /* ------------------------------------- GF(2^w) scalar ops (host only) --- */

@@ -55,3 +55,23 @@ def gpu():
     assert torch.cuda.is_available(), "GPU tests need an MI355X (run with -m gpu on the GPU box)"
     import erasure_coding_test_amd  # noqa: F401
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def knobs():
+    """The library's tuning knobs (ecgpu_set_knob), restored after the test:
+    the environment is read once per process, so in-process switches go
+    through the setter."""
+    from erasure_coding_test_amd import _native as N
+
+    class Knobs:
+        @staticmethod
+        def set(name, value):
+            N.set_knob(name, int(value))
+
+        @staticmethod
+        def reset(name):
+            N.reset_knob(name)
+
+    yield Knobs()
+    N.reset_knob(None)

@@ -581,16 +581,12 @@ def test_host_pipeline_mixed_output_memory(ec, gpu, restatement, pattern):
 
 
 @pytest.fixture
-def d2h_worker_delay():
-    """ECGPU_TEST_D2H_DELAY_US: the pipeline's D2H worker sleeps 3 ms between
-    taking a job and issuing it (read when a pipeline is created)."""
-    old = os.environ.get("ECGPU_TEST_D2H_DELAY_US")
-    os.environ["ECGPU_TEST_D2H_DELAY_US"] = "3000"
+def d2h_worker_delay(knobs):
+    """The test_d2h_delay_us knob (a test hook with no environment variable):
+    the pipeline's D2H worker sleeps 3 ms between taking a job and issuing it
+    (read when a pipeline is created)."""
+    knobs.set("test_d2h_delay_us", 3000)
     yield
-    if old is None:
-        del os.environ["ECGPU_TEST_D2H_DELAY_US"]
-    else:
-        os.environ["ECGPU_TEST_D2H_DELAY_US"] = old
 
 
 @pytest.mark.parametrize("pattern", ["alternate", "pageable_then_pinned"])
@@ -935,7 +931,7 @@ def test_wide_word_matrix_coding_device(ec, gpu, w, size, offset):
 @pytest.mark.parametrize("w", [16, 32])
 @pytest.mark.parametrize("engine", ["nib", "perm"])
 @pytest.mark.parametrize("k,m", [(3, 1), (5, 2), (7, 3), (9, 7), (33, 4), (40, 5)])
-def test_wide_word_random_matrix_engines(ec, gpu, monkeypatch, w, engine, k, m):
+def test_wide_word_random_matrix_engines(ec, gpu, knobs, w, engine, k, m):
     """Random w = 16 / 32 coding matrices (zeros, units and general
     coefficients) through both column engines -- LDS nibble tables
     (gf_apply_wide_nib; k = 33 / 40 with 4 rows exceed its LDS budget and
@@ -943,9 +939,9 @@ def test_wide_word_random_matrix_engines(ec, gpu, monkeypatch, w, engine, k, m):
     1..4 rows per launch and a second launch for m > 4."""
     import torch
     if engine == "perm":
-        monkeypatch.setenv("ECGPU_WIDE", "1")
+        knobs.set("ECGPU_WIDE", "1")
     else:
-        monkeypatch.delenv("ECGPU_WIDE", raising=False)
+        knobs.reset("ECGPU_WIDE")
     ref = _ref_nsa()
     rng = np.random.default_rng(1000 * w + 10 * k + m)
     hi = (1 << w) - 1
@@ -968,7 +964,7 @@ def test_wide_word_random_matrix_engines(ec, gpu, monkeypatch, w, engine, k, m):
 @pytest.mark.parametrize("w,nib16", [(32, "1"), (16, "0")])
 @pytest.mark.parametrize("units", ["1", "0"])
 @pytest.mark.parametrize("k,m", [(10, 4), (6, 2), (5, 3), (32, 4), (12, 6), (2, 2)])
-def test_wide_word_unit_structured_launches(ec, gpu, monkeypatch, w, nib16, units, k, m):
+def test_wide_word_unit_structured_launches(ec, gpu, knobs, w, nib16, units, k, m):
     """Launches whose row 0 and column 0 are all ones (every Vandermonde
     encode) run gf_apply_wide_nib<R, 1>: row 0 and source 0 by XOR, the other
     rows of sources 1..K-1 from LDS (R = 2, 3, 4; m = 6 is a unit launch of
@@ -976,9 +972,9 @@ def test_wide_word_unit_structured_launches(ec, gpu, monkeypatch, w, nib16, unit
     with zeros and units mixed in, against the reference library, with the
     unit form on and off (ECGPU_WIDE_UNITS)."""
     import torch
-    monkeypatch.delenv("ECGPU_WIDE", raising=False)
-    monkeypatch.setenv("ECGPU_NIB16", nib16)
-    monkeypatch.setenv("ECGPU_WIDE_UNITS", units)
+    knobs.reset("ECGPU_WIDE")
+    knobs.set("ECGPU_NIB16", nib16)
+    knobs.set("ECGPU_WIDE_UNITS", units)
     ref = _ref_nsa()
     rng = np.random.default_rng(77 * w + 10 * k + m)
     hi = (1 << w) - 1
@@ -1015,7 +1011,7 @@ _PIPE_CASES = [(k, m, 3) for k, m in _PIPE_SHAPES] + [(k, m, 1600) for k, m in (
 @pytest.mark.parametrize("structure", ["vandermonde", "random"])
 @pytest.mark.parametrize("k,m,blocks", _PIPE_CASES)
 @pytest.mark.parametrize("pipe", ["2", "1"])
-def test_wide_word_pipelined_launches(ec, gpu, monkeypatch, w, structure, k, m, blocks, pipe):
+def test_wide_word_pipelined_launches(ec, gpu, knobs, w, structure, k, m, blocks, pipe):
     """Launches of whole 256-column blocks (4 KiB per shard each) run
     gf_apply_wide_pipe<K, R, mode> -- compile-time K, double-buffered source
     chunks, all three modes (w = 32 unit structure, w = 32 general, w = 16
@@ -1025,10 +1021,10 @@ def test_wide_word_pipelined_launches(ec, gpu, monkeypatch, w, structure, k, m, 
     one resident round).  Encode and a decode of up to m erasures against the
     reference library."""
     import torch
-    monkeypatch.delenv("ECGPU_WIDE", raising=False)
-    monkeypatch.delenv("ECGPU_NIB16", raising=False)
-    monkeypatch.delenv("ECGPU_WIDE_UNITS", raising=False)
-    monkeypatch.setenv("ECGPU_WIDE_PIPE", pipe)
+    knobs.reset("ECGPU_WIDE")
+    knobs.reset("ECGPU_NIB16")
+    knobs.reset("ECGPU_WIDE_UNITS")
+    knobs.set("ECGPU_WIDE_PIPE", pipe)
     ref = _ref_nsa()
     rng = np.random.default_rng(31 * w + 7 * k + m + blocks)
     if structure == "vandermonde":
@@ -1148,14 +1144,14 @@ def test_bitmatrix_coding_device(ec, gpu, k, m, w, ps):
 @pytest.mark.parametrize("kind", ["0", "1", "2"])  # ECGPU_PACKET: pipelined 16-B, 8-B lanes, unpipelined 16-B
 @pytest.mark.parametrize("k,m,w,ps", [(1, 1, 3, 64), (5, 2, 3, 128), (3, 2, 5, 16), (10, 4, 8, 2048),
                                       (7, 5, 2, 48), (4, 3, 3, 8), (3, 3, 3, 5)])
-def test_random_bitmatrix_packet_kernels(ec, gpu, monkeypatch, kind, k, m, w, ps):
+def test_random_bitmatrix_packet_kernels(ec, gpu, knobs, kind, k, m, w, ps):
     """A random 0/1 bit-matrix (any w) through jerasure_bitmatrix_encode on
     every packet kernel: source-row counts below one pipelined chunk of four
     (k*w = 3), with a ragged tail (15), and whole chunks (80); 16-B, 8-B and
     byte packets; more than 8 / 16 output rows; all-zero rows leave their
     output packets untouched, as the reference does."""
     import torch
-    monkeypatch.setenv("ECGPU_PACKET", kind)
+    knobs.set("ECGPU_PACKET", kind)
     rng = np.random.default_rng(k * 131 + m * 17 + w * 5 + ps)
     bm = [int(b) for b in rng.integers(0, 2, k * w * m * w)]
     size = w * ps * 7

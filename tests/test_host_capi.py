@@ -191,20 +191,53 @@ def test_recommended_stride():
         assert st(size) % 256 == 0 and st(size) >= size
 
 
-def test_stride_skew_override(monkeypatch):
-    """ECGPU_SHARD_SKEW_KIB replaces the per-size table (read per call);
-    malformed or out-of-range values are ignored."""
+def test_stride_skew_override(knobs):
+    """The shard_skew_kib knob (ECGPU_SHARD_SKEW_KIB) replaces the per-size
+    table; values outside 0..1024 are ignored."""
     from erasure_coding_test_amd import _native as N
     st = N.lib.ecgpu_recommended_shard_stride
-    monkeypatch.setenv("ECGPU_SHARD_SKEW_KIB", "12")
+    knobs.set("ECGPU_SHARD_SKEW_KIB", 12)
     assert st(4 << 20) == (4 << 20) + (12 << 10) and st(1 << 20) == (1 << 20) + (12 << 10)
-    monkeypatch.setenv("ECGPU_SHARD_SKEW_KIB", "0")
+    knobs.set("shard_skew_kib", 0)
     assert st(16 << 20) == 16 << 20
-    for bad in ("", "x", "12k", "-4", "2000"):
-        monkeypatch.setenv("ECGPU_SHARD_SKEW_KIB", bad)
+    for bad in (-4, 2000):
+        knobs.set("ECGPU_SHARD_SKEW_KIB", bad)
         assert st(4 << 20) == (4 << 20) + (6 << 10), bad
-    monkeypatch.delenv("ECGPU_SHARD_SKEW_KIB")
+    knobs.reset("ECGPU_SHARD_SKEW_KIB")
     assert st(4 << 20) == (4 << 20) + (6 << 10)
+
+
+KNOB_ENV = """
+import os, sys
+sys.path.insert(0, {root!r})
+from erasure_coding_test_amd import _native as N
+print(N.get_knob("ECGPU_SHARD_SKEW_KIB"), N.lib.ecgpu_recommended_shard_stride(4 << 20) - (4 << 20))
+"""
+
+
+@pytest.mark.parametrize("env,want", [("12", "12 12288"), ("", "-1 6144"), ("x", "-1 6144"), ("12k", "-1 6144"),
+                                      ("-4", "-4 6144"), ("2000", "2000 6144")])
+def test_knob_environment_is_read_once_and_strictly(env, want):
+    """The environment is read once, at first use, as a whole decimal integer:
+    a malformed value keeps the default."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ, ECGPU_SHARD_SKEW_KIB=env)
+    r = subprocess.run([sys.executable, "-c", KNOB_ENV.format(root=root)], capture_output=True, text=True, env=e,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split("\n")[-2] == want
+
+
+def test_knobs_set_get_reset():
+    from erasure_coding_test_amd import _native as N
+    assert N.get_knob("cap") == N.get_knob("ECGPU_CAP")
+    N.set_knob("ECGPU_CAP", 0)
+    assert N.get_knob("cap") == 0
+    N.reset_knob("cap")
+    assert N.get_knob("ECGPU_CAP") == -1
+    with pytest.raises(N.EcgpuError, match="unknown knob"):
+        N.set_knob("ECGPU_NOPE", 1)
+    assert N.lib.ecgpu_set_knob(b"cap", -(2**31)) == N.ECGPU_ERR_ARG  # the reserved "unset" value
 
 
 NO_GPU = not os.path.exists("/dev/kfd")

@@ -28,6 +28,7 @@ def run():
     import torch
 
     import erasure_coding_test_amd as E
+    from erasure_coding_test_amd import _native as N
     k, m, w, S = 10, 4, 16, 64 << 20
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w)
     sep_d = [torch.randint(0, 256, (S,), dtype=torch.uint8, device="cuda") for _ in range(k)]
@@ -39,7 +40,7 @@ def run():
         for L in LAYOUTS:
             d, c = lay[L]
             for st in SETTINGS:
-                os.environ["ECGPU_WIDE16_BPCU"] = st
+                N.set_knob("ECGPU_WIDE16_BPCU", int(st))
                 for _ in range(REPS):
                     E.jerasure.jerasure_matrix_encode(k, m, w, M, d, c, S)
     torch.cuda.synchronize()

@@ -21,6 +21,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import erasure_coding_test_amd as E  # noqa: E402
+from erasure_coding_test_amd import _native as N  # noqa: E402
 
 
 def timed(fn, reps):
@@ -54,11 +55,11 @@ def main():
     for w in (8, 16, 32):
         M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w)
         rec(f"jerasure_matrix_encode w={w}", lambda M=M, w=w: J.jerasure_matrix_encode(k, m, w, M, data, coding, S))
-        if w != 8:  # A/B: the v_perm column engine (read per launch by the runtime)
-            os.environ["ECGPU_WIDE"] = "1"
+        if w != 8:  # A/B: the v_perm column engine (a knob, switched in process)
+            N.set_knob("ECGPU_WIDE", 1)
             rec(f"jerasure_matrix_encode w={w} (v_perm engine, ECGPU_WIDE=1)",
                 lambda M=M, w=w: J.jerasure_matrix_encode(k, m, w, M, data, coding, S))
-            del os.environ["ECGPU_WIDE"]
+            N.reset_knob("ECGPU_WIDE")
     M8 = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     # the same shards through the batched plan API (gf_apply, pointer and
     # coefficient tables in HBM) against the synchronous call's inline launch

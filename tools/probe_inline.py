@@ -16,6 +16,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import erasure_coding_test_amd as E  # noqa: E402
+from erasure_coding_test_amd import _native as N  # noqa: E402
 
 
 def main():
@@ -29,7 +30,7 @@ def main():
         ref = None
         for rnd in range(3):
             for inl in ("1", "0"):
-                os.environ["ECGPU_INLINE"] = inl
+                N.set_knob("ECGPU_INLINE", int(inl))
                 for _ in range(5):
                     E.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, S)
                 torch.cuda.synchronize()

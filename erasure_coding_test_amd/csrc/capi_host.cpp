@@ -1,6 +1,7 @@
 // capi_host.cpp -- host-only entry points of include/ecgpu.h (no GPU touched).
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "ecgpu.h"
@@ -12,9 +13,23 @@
 
 using namespace ecgpu;
 
+namespace ecgpu {
+namespace __attribute__((visibility("hidden"))) rt {
+// The thread's last error message (ecgpu_last_error); every translation unit
+// of the library reports through fail().
+thread_local std::string t_err;
+
+int fail(int code, const std::string& msg) {
+  t_err = msg;
+  return code;
+}
+}  // namespace rt
+}  // namespace ecgpu
+
 extern "C" {
 
 ECGPU_API const char* ecgpu_version(void) { return "ecgpu 0.1 (gfx950)"; }
+ECGPU_API const char* ecgpu_last_error(void) { return rt::t_err.c_str(); }
 
 // Content IDs of this build (erasure_coding_test_amd/build.py): 0 the whole
 // library, 1 the coding kernels and their dispatch.

@@ -52,12 +52,8 @@ using dev::u32x4;
 
 ECGPU_RT_BEGIN
 
-thread_local std::string t_err;
-
-int fail(int code, const std::string& msg) {
-  t_err = msg;
-  return code;
-}
+// t_err / fail / ecgpu_last_error live in capi_host.cpp (host code, so the
+// host-only checks -- buffer contract, knobs -- report through them too)
 
 
 // ------------------------------------------------------- kernel tables ----
@@ -1167,7 +1163,6 @@ ECGPU_RT_END
 // ================================================================ C ABI ====
 extern "C" {
 
-ECGPU_API const char* ecgpu_last_error(void) { return t_err.c_str(); }
 
 ECGPU_API ecgpu_plan* ecgpu_plan_create(int rows, int nsrc, const int* coefs, int device) {
   if (rows <= 0 || nsrc <= 0 || !coefs) {

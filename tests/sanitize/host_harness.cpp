@@ -1,7 +1,7 @@
 // host_harness.cpp -- drives the HOST-ONLY part of libecgpu (field tables,
 // matrix construction / inversion, the decode planner, bit-matrix and
-// schedule construction; csrc/{gf_host,matrix_host,planner,schedule_host,
-// capi_host}.cpp) under AddressSanitizer + UBSan, or ThreadSanitizer with
+// schedule construction, the buffer contract, knobs; csrc/{gf_host,
+// matrix_host,planner,schedule_host,capi_host,contract_host,knobs}.cpp) under AddressSanitizer + UBSan, or ThreadSanitizer with
 // `threads` > 1 (first-use table initialisation races between callers).
 // Built and run by tests/test_sanitizers.py.  No GPU code is linked: the one
 // device entry point the host objects reference is stubbed and never called.
@@ -9,6 +9,7 @@
 //   host_harness [threads]      exit 0 = every check passed, sanitizer clean
 #include <cstdio>
 #include <cstdlib>
+#include <cstdint>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -116,10 +117,58 @@ void decode_plans() {
   std::free(M);
 }
 
+// The buffer contract of the plan API (contract_host.cpp): random binds
+// against the pairwise rule, so the sweep's sort / groups run under the
+// sanitizers and concurrently.
+void buffer_contract(unsigned seed) {
+  for (int trial = 0; trial < 300; ++trial) {
+    seed = seed * 1103515245u + 12345u;
+    const int rows = 1 + int(seed >> 8) % 6, nsrc = 1 + int(seed >> 12) % 5, stripes = 1 + int(seed >> 16) % 4;
+    const int64_t size = 1 + int64_t(seed >> 20) % 100;
+    std::vector<uint8_t*> src(size_t(stripes * nsrc)), dst(size_t(stripes * rows));
+    auto pick = [&]() {
+      seed = seed * 1103515245u + 12345u;
+      return reinterpret_cast<uint8_t*>(uintptr_t(1) << 20) + (seed >> 16) % 400;
+    };
+    for (auto& p : src) p = pick();
+    for (auto& p : dst) p = pick();
+    bool ok = true;  // the pairwise rule
+    const int per = nsrc + rows;
+    for (int i = 0; i < stripes * per && ok; ++i)
+      for (int j = i + 1; j < stripes * per && ok; ++j) {
+        const int si = i / per, sj = j / per, ii = i % per, jj = j % per;
+        const bool wi = ii >= nsrc, wj = jj >= nsrc;
+        if (!wi && !wj) continue;
+        const uint8_t* p = wi ? dst[size_t(si * rows + ii - nsrc)] : src[size_t(si * nsrc + ii)];
+        const uint8_t* q = wj ? dst[size_t(sj * rows + jj - nsrc)] : src[size_t(sj * nsrc + jj)];
+        if (!(p < q + size && q < p + size)) continue;
+        if (p == q && wi != wj && si == sj && rows <= 4) continue;
+        ok = false;
+      }
+    const int rc = ecgpu_plan_check_buffers(rows, nsrc, stripes, const_cast<const uint8_t* const*>(src.data()),
+                                            dst.data(), size);
+    expect((rc == ECGPU_OK) == ok, "plan buffer contract", trial, rc);
+    if (rc != ECGPU_OK) expect(std::strstr(ecgpu_last_error(), "overlap") != nullptr, "contract message", trial);
+  }
+}
+
+// Knobs set and read from several threads; the split tables built once.
+void knobs_and_split_tables() {
+  int v = 0;
+  expect(ecgpu_get_knob("ECGPU_CAP", &v) == ECGPU_OK, "get knob");
+  expect(ecgpu_set_knob("ECGPU_NOT_A_KNOB", 1) == ECGPU_ERR_ARG, "unknown knob");
+  expect(ecgpu_galois_create_split_w8_tables() == 0, "split tables");
+  for (int x : {0, 1, 255, 0x12345678, -1})
+    expect(ecgpu_galois_split_w8_multiply(x, 0x0BADF00D) == ecgpu_galois_single_multiply(x, 0x0BADF00D, 32),
+           "split multiply", x);
+}
+
 void run_all() {
+  knobs_and_split_tables();
   known_answers();
   matrices();
   decode_plans();
+  buffer_contract(0xEC5u);
 }
 
 }  // namespace

@@ -30,7 +30,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "erasure_coding_test_amd", "csrc")
-HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp"]
+HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp", "contract_host.cpp",
+             "knobs.cpp"]
 HARNESS = os.path.join(ROOT, "tests", "sanitize", "host_harness.cpp")
 PIPE_HARNESS = os.path.join(ROOT, "tests", "sanitize", "pipeline_harness.cpp")
 TSAN_ENV = {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}

@@ -7,6 +7,7 @@
 #include "ecgpu.h"
 #include "gf_host.hpp"
 #include "knobs.hpp"
+#include "shard_stride.hpp"
 #include "matrix_host.hpp"
 #include "planner.hpp"
 #include "schedule_host.hpp"
@@ -42,34 +43,7 @@ ECGPU_API const char* ecgpu_last_error(void) { return rt::t_err.c_str(); }
 ECGPU_API const char* ecgpu_build_id(int what) { return what == 1 ? ECGPU_KERNEL_ID : ECGPU_BUILD_ID; }
 ECGPU_API void ecgpu_free(void* p) { std::free(p); }
 
-// Shard-stride skew.  A lane reads the same column of every shard, so the
-// k + m concurrent accesses sit one stride apart; when that stride lines up
-// with the HBM channel / bank hash they collide.  The effect is a
-// deterministic function of the stride: an in-process sweep (RS(10,4), ~5 GiB
-// per launch, every skew's slab interleaved, tools/skew_sweep.sh) gave the same
-// numbers within ~1 % on three MI355X boxes (profiles/r03_skew_sweep_*.jsonl),
-// including sharp dips of 15-30 % (e.g. +12 KiB at 1 and 3 MiB shards, +8 KiB
-// at 2 and 6 MiB, +14 KiB at 512 KiB, no skew from 4 MiB up), and again on
-// independent random shards (profiles/r03_skew_sweep_random.jsonl; the first
-// sweeps filled every shard from one buffer, and HBM throughput depends on the
-// data).  For the shard sizes measured, the skew with the best
-// rate; tie-breaks from the BASELINE configs' own A/Bs on random data:
-// RS(6,3) 1 MiB none (1-3 % over +10 KiB, profiles/r03_skew_ab_random.jsonl);
-// RS(10,4) 4 MiB +6 KiB, the best bench step (encode + decode{0}) on three
-// boxes, 0.6-1 % over the +14 KiB first chosen on the old fill
-// (profiles/r03_skew_step_ab.jsonl); RS(12,4) 16 MiB +8 KiB (4 %).  Other
-// sizes keep +10 KiB, within 1-4 % of the best at every size measured and
-// never near a dip.
-struct SkewClass {
-  int64_t size, skew;
-};
-constexpr SkewClass kSkewTable[] = {
-    {256 << 10, 12 << 10}, {512 << 10, 8 << 10},  {1 << 20, 0},          {2 << 20, 12 << 10},
-    {3 << 20, 8 << 10},    {4 << 20, 6 << 10},   {6 << 20, 12 << 10},   {8 << 20, 12 << 10},
-    {12 << 20, 8 << 10},   {16 << 20, 8 << 10},   {32 << 20, 8 << 10},   {64 << 20, 8 << 10},
-};
-constexpr int64_t kDefaultSkew = 10 << 10;
-
+// The shard stride of shard_stride.hpp (the measured per-size skew table).
 ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size) {
   if (size < 0) size = 0;
   const int64_t rounded = (size + 255) & ~int64_t(255);
@@ -77,10 +51,7 @@ ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size) {
   // (A/B runs of whole workloads); outside 0..1024 the table applies
   const int v = knob(Knob::kShardSkewKib);
   if (v >= 0 && v <= 1024) return rounded + int64_t(v) * 1024;
-  int64_t skew = kDefaultSkew;
-  for (const SkewClass& c : kSkewTable)
-    if (rounded >= c.size - c.size / 16 && rounded <= c.size + c.size / 16) skew = c.skew;
-  return rounded + skew;
+  return shard_stride(size);
 }
 
 ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w) { return single_multiply(a, b, w); }

@@ -1424,15 +1424,16 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
 // (profiles/r03_wide_lab.jsonl, runs "r03 pipe ...").
 enum WidePipeMode : int { kPipeW32 = 0, kPipeW32Unit = 1, kPipeW16 = 2 };
 
-template <int K, int MODE>
+template <int K, int MODE, int NCHO = 0>
 struct WidePipeShape {
   // chunks per column: w = 32 four for K = 7..12 (RS(10,4): 3 + 3 + 3 + 1,
-  // 101 VGPRs, 4 workgroups per CU), w = 16 two (5 + 5)
-  static constexpr int NCH = MODE == kPipeW16 ? 2 : 2 * ((K + 5) / 6);
+  // 101 VGPRs, 4 workgroups per CU), w = 16 two (5 + 5); NCHO > 0 overrides
+  // (even)
+  static constexpr int NCH = NCHO > 0 ? NCHO : MODE == kPipeW16 ? 2 : 2 * ((K + 5) / 6);
   static constexpr int CH = (K + NCH - 1) / NCH;
 };
 
-template <int K, int R, int MODE, int WPE = 1>
+template <int K, int R, int MODE, int WPE = 1, int NCHO = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_apply_wide_pipe(ApplyArgs a) {
   constexpr bool W16 = MODE == kPipeW16;
   constexpr int U = MODE == kPipeW32Unit ? 1 : 0;
@@ -1440,7 +1441,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   constexpr int L = R - U;  // rows looked up (w = 32)
   constexpr int EW = W16 ? nib16_entry_words(R) : nib_entry_words(L), EB = 4 * EW;
   constexpr uint32_t kSrcBytes = uint32_t(W16 ? nib16_source_bytes(R) : nib_source_bytes(L));
-  constexpr int NCH = WidePipeShape<K, MODE>::NCH, CH = WidePipeShape<K, MODE>::CH;
+  constexpr int NCH = WidePipeShape<K, MODE, NCHO>::NCH, CH = WidePipeShape<K, MODE, NCHO>::CH;
   static_assert(NCH % 2 == 0, "buffer parity repeats per column");
   extern __shared__ __attribute__((aligned(16))) uint8_t nib_lds[];
   {

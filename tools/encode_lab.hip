@@ -9,7 +9,7 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I erasure_coding_test_amd/csrc \
 //     tools/encode_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp erasure_coding_test_amd/csrc/matrix_host.cpp \
 //     -o tools/encode_lab.bin
-//   tools/encode_lab.bin [--stripes 96] [--rounds 7] [--reps 10]
+//   tools/encode_lab.bin [--stripes 96] [--rounds 7] [--reps 10] [--skew-kib N]
 //   tools/encode_lab.bin --skews 10,12,8,6 [--k 12 --m 4 --mib 16 --stripes 24]
 //       the production launch on one slab per shard-stride skew (KiB), interleaved
 #include <hip/hip_runtime.h>
@@ -25,6 +25,7 @@
 #include "gf_host.hpp"
 #include "gf_kernels.hpp"
 #include "matrix_host.hpp"
+#include "shard_stride.hpp"
 
 using namespace ecgpu;
 using namespace ecgpu::dev;
@@ -189,7 +190,7 @@ template <int k, int m>
 int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int reps);
 
 int main(int argc, char** argv) {
-  int stripes = 96, rounds = 7, reps = 10, kk = 10, mm = 4, kib = 4096;
+  int stripes = 96, rounds = 7, reps = 10, kk = 10, mm = 4, kib = 4096, skew_kib = -1;
   std::vector<int> skews;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string f = argv[i];
@@ -203,6 +204,7 @@ int main(int argc, char** argv) {
     else if (f == "--early0") g_early0 = std::atoi(argv[i + 1]) != 0;
     else if (f == "--vec2") g_vec2 = std::atoi(argv[i + 1]) != 0;
     else if (f == "--dense") g_dense = std::atoi(argv[i + 1]) != 0;
+    else if (f == "--skew-kib") skew_kib = std::atoi(argv[i + 1]);
     else if (f == "--skews") {
       std::string v = argv[i + 1];
       size_t p = 0;
@@ -223,7 +225,9 @@ int main(int argc, char** argv) {
     return 2;
   }
   constexpr int k = 10, m = 4;
-  const size_t S = size_t(4) << 20, stride = S + (10 << 10);
+  // the library's stride for 4 MiB shards (shard_stride.hpp), or --skew-kib
+  const size_t S = size_t(4) << 20;
+  const size_t stride = skew_kib >= 0 ? S + size_t(skew_kib) * 1024 : size_t(shard_stride(int64_t(S)));
   int* M = vandermonde_coding_matrix(k, m, 8);
   if (g_dense) {
     std::mt19937 gm(4);

@@ -9,7 +9,7 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I erasure_coding_test_amd/csrc \
 //     tools/packet_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp erasure_coding_test_amd/csrc/matrix_host.cpp \
 //     -o tools/packet_lab.bin
-//   tools/packet_lab.bin [--mib 64] [--ps 4096] [--rounds 9] [--reps 10]
+//   tools/packet_lab.bin [--mib 64] [--ps 4096] [--rounds 9] [--reps 10] [--skew-kib N]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -24,6 +24,7 @@
 #include "gf_host.hpp"
 #include "gf_kernels.hpp"
 #include "matrix_host.hpp"
+#include "shard_stride.hpp"
 
 using namespace ecgpu;
 using namespace ecgpu::dev;
@@ -251,16 +252,19 @@ struct Variant {
 };
 
 int main(int argc, char** argv) {
-  int mib = 64, ps = 4096, rounds = 9, reps = 10;
+  int mib = 64, ps = 4096, rounds = 9, reps = 10, skew_kib = -1;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string f = argv[i];
     if (f == "--mib") mib = std::atoi(argv[i + 1]);
     else if (f == "--ps") ps = std::atoi(argv[i + 1]);
     else if (f == "--rounds") rounds = std::atoi(argv[i + 1]);
     else if (f == "--reps") reps = std::atoi(argv[i + 1]);
+    else if (f == "--skew-kib") skew_kib = std::atoi(argv[i + 1]);
   }
   const int k = 10, m = 4, w = 8;
-  const size_t S = size_t(mib) << 20, stride = S + (10 << 10);
+  // the library's stride (shard_stride.hpp), or --skew-kib
+  const size_t S = size_t(mib) << 20;
+  const size_t stride = skew_kib >= 0 ? S + size_t(skew_kib) * 1024 : size_t(shard_stride(int64_t(S)));
   if (S % (size_t(w) * ps) || ps % 16) {
     std::fprintf(stderr, "S must be a multiple of w * ps, ps of 16\n");
     return 2;

@@ -6,7 +6,7 @@
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I erasure_coding_test_amd/csrc \
 //     tools/wide_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp erasure_coding_test_amd/csrc/matrix_host.cpp -o tools/wide_lab.bin
-//   tools/wide_lab.bin [--w 32] [--k 10] [--m 4] [--mib 64] [--rounds 7] [--reps 10] [--only name,name]
+//   tools/wide_lab.bin [--w 32] [--k 10] [--m 4] [--mib 64] [--rounds 7] [--reps 10] [--only name,name] [--skew-kib N]
 //
 // Prints one JSON line per variant: median / min us and GB/s of (k+m)*S.
 #include <hip/hip_runtime.h>
@@ -24,6 +24,7 @@
 #include "gf_host.hpp"
 #include "gf_kernels.hpp"
 #include "matrix_host.hpp"
+#include "shard_stride.hpp"
 
 using namespace ecgpu;
 using namespace ecgpu::dev;
@@ -386,7 +387,7 @@ struct Variant {
 };
 
 int main(int argc, char** argv) {
-  int w = 32, k = 10, m = 4, mib = 64, rounds = 7, reps = 10;
+  int w = 32, k = 10, m = 4, mib = 64, rounds = 7, reps = 10, skew_kib = -1;
   std::string only;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string f = argv[i];
@@ -397,12 +398,15 @@ int main(int argc, char** argv) {
     else if (f == "--rounds") rounds = std::atoi(argv[i + 1]);
     else if (f == "--reps") reps = std::atoi(argv[i + 1]);
     else if (f == "--only") only = argv[i + 1];
+    else if (f == "--skew-kib") skew_kib = std::atoi(argv[i + 1]);
   }
   if (m != 4 || k < 2 || k > 16 || (w != 32 && w != 16)) {
     std::fprintf(stderr, "lab covers m = 4, 2 <= k <= 16, w = 16 / 32\n");
     return 2;
   }
-  const size_t S = size_t(mib) << 20, stride = S + (10 << 10);
+  // the library's stride (shard_stride.hpp: +8 KiB at 64 MiB), or --skew-kib
+  const size_t S = size_t(mib) << 20;
+  const size_t stride = skew_kib >= 0 ? S + size_t(skew_kib) * 1024 : size_t(shard_stride(int64_t(S)));
   const int R = m, K = k;
   // Vandermonde coding matrix of the reference (reed_sol.cpp:63-84)
   int* M = vandermonde_coding_matrix(k, m, w);

@@ -422,16 +422,23 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
     const int R = std::min(dev::kMaxRows, p->rows - r0);
     // w = 16 packs two rows per LDS dword (gf_apply_wide_nib16, half the LDS bytes)
     const bool pack16 = W == 2 && knob(Knob::kNib16) != 0;
-    // the 32-bit-entry kernel's unit structure (gf_apply_wide_nib<R, 1>): the
-    // launch's row 0 and column 0 all ones, as in every Vandermonde encode
-    bool unit_rc = !pack16 && R >= 2 && knob(Knob::kWideUnits) != 0;
+    // the unit structure (gf_apply_wide_nib<R, 1>, gf_apply_wide_nib16<R, 1>):
+    // the launch's row 0 and column 0 all ones, as in every Vandermonde encode
+    bool unit_rc = R >= 2 && knob(pack16 ? Knob::kWide16Units : Knob::kWideUnits) != 0;
     for (int j = 0; j < K && unit_rc; ++j) unit_rc = p->coef[size_t(r0) * K + j] == 1u;
     for (int r = 0; r < R && unit_rc; ++r) unit_rc = p->coef[size_t(r0 + r) * K] == 1u;
-    const unsigned nib_lds = pack16 ? unsigned(K) * unsigned(dev::nib16_source_bytes(R))
-                                    : unsigned(dev::nib_lds_bytes(K, R, unit_rc ? 1 : 0));
+    const unsigned nib_lds =
+        pack16 ? unsigned(K - (unit_rc ? 1 : 0)) * unsigned(dev::nib16_source_bytes(R - (unit_rc ? 1 : 0)))
+               : unsigned(dev::nib_lds_bytes(K, R, unit_rc ? 1 : 0));
     const bool nib = !force_perm && nib_lds <= unsigned(dev::kNibMaxLds);
     KernelFn vec_fn = nullptr, word_fn = W == 2 ? &dev::gf_apply_wide_words<2> : &dev::gf_apply_wide_words<4>;
-    if (nib && pack16) {
+    if (nib && pack16 && unit_rc) {
+      switch (R) {
+        case 2: vec_fn = &dev::gf_apply_wide_nib16<2, 1>; break;
+        case 3: vec_fn = &dev::gf_apply_wide_nib16<3, 1>; break;
+        default: vec_fn = &dev::gf_apply_wide_nib16<4, 1>; break;
+      }
+    } else if (nib && pack16) {
       switch (R) {
         case 1: vec_fn = &dev::gf_apply_wide_nib16<1>; break;
         case 2: vec_fn = &dev::gf_apply_wide_nib16<2>; break;
@@ -469,10 +476,16 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
     // ECGPU_WIDE_PIPE: 1 that rule (default), 0 never, 2 every whole-block
     // launch of every mode (tests, A/B).
     const int pipe = knob(Knob::kWidePipe);
+    // (the pipelined w = 16 form has no unit structure: it packs every row)
     const bool pipe_shape = pipe == 2 || (pipe == 1 && !pack16 && unit_rc && K >= 7 && K <= 10);
+    bool piped = false;
     if (nib && nvec > 0 && nvec % dev::kBlock == 0 && pipe_shape)
-      if (KernelFn f = wide_pipe_kernel(K, R, pack16 ? dev::kPipeW16 : unit_rc ? dev::kPipeW32Unit : dev::kPipeW32))
+      if (KernelFn f = wide_pipe_kernel(K, R, pack16 ? dev::kPipeW16 : unit_rc ? dev::kPipeW32Unit : dev::kPipeW32)) {
         vec_fn = f;
+        piped = true;
+      }
+    const unsigned launch_lds =
+        piped && pack16 && unit_rc ? unsigned(K) * unsigned(dev::nib16_source_bytes(R)) : nib_lds;
     for (int s0 = 0; s0 < p->stripes; s0 += kMaxGridY) {
       const int ns = std::min(kMaxGridY, p->stripes - s0);
       ApplyArgs a{};
@@ -503,14 +516,14 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
           // profiles/r03_wide_lab.jsonl); the LDS-bound w = 32 kernel wants
           // every wave it can get (3 per CU: 242 vs 192 us).
           // ECGPU_WIDE16_BPCU overrides (0: the occupancy).
-          int bpcu = resident_blocks(vec_fn, nib_lds);
+          int bpcu = resident_blocks(vec_fn, launch_lds);
           if (pack16) {
             const int cap16 = knob(Knob::kWide16Bpcu);
             if (cap16 > 0) bpcu = std::min(bpcu, cap16);
           }
           const int64_t per_stripe = std::max<int64_t>(1, int64_t(multiprocessors(p->device)) * bpcu / ns);
           const dim3 grid(unsigned(std::min(nblk, per_stripe)), unsigned(ns));
-          ECGPU_HIP(launch(vec_fn, grid, block, a, stream, nib_lds));
+          ECGPU_HIP(launch(vec_fn, grid, block, a, stream, launch_lds));
         } else {
           ECGPU_HIP(launch(vec_fn, dim3(unsigned(nblk), unsigned(ns)), block, a, stream));
         }

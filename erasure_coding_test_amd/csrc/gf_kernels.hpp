@@ -1320,21 +1320,29 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib(ApplyArgs a) {
 __host__ __device__ constexpr int nib16_entry_words(int R) { return R <= 2 ? 1 : 2; }
 __host__ __device__ constexpr int nib16_source_bytes(int R) { return kNibWords * 4 * nib16_entry_words(R); }
 
-template <int R>
+// U = 1: the unit structure of gf_apply_wide_nib<R, 1> (the launch's row 0
+// and column 0 all ones, as in every Vandermonde encode): row 0 is the XOR of
+// the sources and source 0 is XORed into every row, so the LDS holds the
+// packed pairs of rows 1..R-1 (pair p = rows 1 + 2p, 2 + 2p) for sources
+// 1..K-1 only -- 1/K fewer lookups, and for R = 3 one dword entry instead of
+// two.  Selected by the wide16_units knob (ECGPU_WIDE16_UNITS).
+template <int R, int U = 0>
 __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
-  constexpr int EW = nib16_entry_words(R), EB = 4 * EW;
+  static_assert(U == 0 || R >= 2, "the unit form needs a row besides the unit row");
+  constexpr int L = R - U;  // rows looked up, packed in pairs
+  constexpr int EW = nib16_entry_words(L), EB = 4 * EW;
   extern __shared__ __attribute__((aligned(16))) uint8_t nib_lds[];
   const int K = a.K;
-  const int n = K * kNibWords * EW;
+  const int n = (K - U) * kNibWords * EW;
   for (int i = threadIdx.x; i < n; i += kBlock) {
-    const int pr = i % EW, e = (i / EW) % kNibWords, j = i / (EW * kNibWords);
+    const int pr = i % EW, e = (i / EW) % kNibWords, j = i / (EW * kNibWords) + U;
     const bool high = (e >> 4) >= 4;  // tables 4..7 hold the high word's products in bits 16..31
     auto word = [&](int r) -> uint32_t {
       if (r >= R) return 0u;
       const uint32_t v = a.wtab[size_t(r * K + j) * kNibWords + e];
       return high ? (v >> 16) : (v & 0xFFFFu);
     };
-    reinterpret_cast<uint32_t*>(nib_lds)[i] = word(2 * pr) | (word(2 * pr + 1) << 16);
+    reinterpret_cast<uint32_t*>(nib_lds)[i] = word(U + 2 * pr) | (word(U + 2 * pr + 1) << 16);
   }
   __syncthreads();
 
@@ -1354,7 +1362,12 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int q = 0; q < EW; ++q) lo[c][q] = hi[c][q] = 0u;
-    for (int j0 = 0; j0 < K; j0 += kChunk) {
+    u32x4 x0 = u32x4{0u, 0u, 0u, 0u}, row0 = u32x4{0u, 0u, 0u, 0u};
+    if constexpr (U == 1) {
+      x0 = load16t<1>(kload(sp, 0), col);  // column 0: into every row
+      row0 = x0;                            // row 0: the XOR of the sources
+    }
+    for (int j0 = U; j0 < K; j0 += kChunk) {
       u32x4 xs[kChunk];
 #pragma unroll
       for (int u = 0; u < kChunk; ++u)
@@ -1363,7 +1376,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
       for (int u = 0; u < kChunk; ++u) {
         const int j = j0 + u;
         if (j >= K) break;
-        const uint32_t jbase = lds_base + uint32_t(j) * uint32_t(nib16_source_bytes(R));
+        if constexpr (U == 1) row0 ^= xs[u];
+        const uint32_t jbase = lds_base + uint32_t(j - U) * uint32_t(nib16_source_bytes(L));
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const uint32_t x = xs[u][c];
@@ -1392,12 +1406,16 @@ __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
         }
       }
     }
+    if constexpr (U == 1) store16t<1>(dp[0], col, row0);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
+    for (int r = U; r < R; ++r) {
+      const int l = r - U;  // looked-up row: pair l / 2, half l % 2
       u32x4 o;
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        o[c] = __builtin_amdgcn_perm(hi[c][r >> 1], lo[c][r >> 1], (r & 1) ? 0x07060302u : 0x05040100u);
+      for (int c = 0; c < 4; ++c) {
+        o[c] = __builtin_amdgcn_perm(hi[c][l >> 1], lo[c][l >> 1], (l & 1) ? 0x07060302u : 0x05040100u);
+        if constexpr (U == 1) o[c] ^= x0[c];
+      }
       store16t<1>(dp[r], col, o);
     }
   }

@@ -22,6 +22,7 @@ enum class Knob : int {
   kWideUnits,       // ECGPU_WIDE_UNITS: w = 32 unit-structure kernel when row 0 / column 0 are ones
   kWidePipe,        // ECGPU_WIDE_PIPE: pipelined wide kernel, 0 never, 1 measured rule, 2 every whole-block launch
   kWide16Bpcu,      // ECGPU_WIDE16_BPCU: w = 16 persistent grid's workgroups per CU (0 = occupancy)
+  kWide16Units,     // ECGPU_WIDE16_UNITS: w = 16 unit-structure kernel (gf_apply_wide_nib16<R, 1>)
   kDevice,          // ECGPU_DEVICE: device of the synchronous calls (-1 = the caller's current device)
   kBounceKib,       // ECGPU_BOUNCE_KIB: staged bytes up to which a call goes through the pinned bounce
   kZcKib,           // ECGPU_ZC_KIB: staged bytes up to which a call is zero-copy

@@ -961,20 +961,22 @@ def test_wide_word_random_matrix_engines(ec, gpu, knobs, w, engine, k, m):
         assert np.array_equal(dc[i].cpu().numpy(), coding[i][:size]), i
 
 
-@pytest.mark.parametrize("w,nib16", [(32, "1"), (16, "0")])
+@pytest.mark.parametrize("w,nib16,unit_knob", [(32, "1", "ECGPU_WIDE_UNITS"), (16, "0", "ECGPU_WIDE_UNITS"),
+                                               (16, "1", "ECGPU_WIDE16_UNITS")])
 @pytest.mark.parametrize("units", ["1", "0"])
-@pytest.mark.parametrize("k,m", [(10, 4), (6, 2), (5, 3), (32, 4), (12, 6), (2, 2)])
-def test_wide_word_unit_structured_launches(ec, gpu, knobs, w, nib16, units, k, m):
+@pytest.mark.parametrize("k,m", [(10, 4), (6, 2), (5, 3), (32, 4), (12, 6), (2, 2), (7, 3)])
+def test_wide_word_unit_structured_launches(ec, gpu, knobs, w, nib16, unit_knob, units, k, m):
     """Launches whose row 0 and column 0 are all ones (every Vandermonde
-    encode) run gf_apply_wide_nib<R, 1>: row 0 and source 0 by XOR, the other
-    rows of sources 1..K-1 from LDS (R = 2, 3, 4; m = 6 is a unit launch of
-    rows 0-3 plus a general launch of rows 4-5).  Random general coefficients
-    with zeros and units mixed in, against the reference library, with the
-    unit form on and off (ECGPU_WIDE_UNITS)."""
+    encode) run the unit forms gf_apply_wide_nib<R, 1> (w = 32, and w = 16
+    with 32-bit entries) and gf_apply_wide_nib16<R, 1> (w = 16 packed pairs):
+    row 0 and source 0 by XOR, the other rows of sources 1..K-1 from LDS
+    (R = 2, 3, 4; m = 6 is a unit launch of rows 0-3 plus a general launch of
+    rows 4-5).  Random general coefficients with zeros and units mixed in,
+    against the reference library, with the unit form on and off."""
     import torch
     knobs.reset("ECGPU_WIDE")
     knobs.set("ECGPU_NIB16", nib16)
-    knobs.set("ECGPU_WIDE_UNITS", units)
+    knobs.set(unit_knob, units)
     ref = _ref_nsa()
     rng = np.random.default_rng(77 * w + 10 * k + m)
     hi = (1 << w) - 1

@@ -1,11 +1,14 @@
-"""In-process A/B of the w = 16 packed nibble kernel's grid cap
-(ECGPU_WIDE16_BPCU, read per launch) on two shard layouts: separately
-allocated 64 MiB tensors (what a caller passing malloc'd shards gets) and the
-library's skewed stripe slab.  Run under rocprofv3 --kernel-trace; launches
-are attributed by order (rounds x layouts x settings x reps).
+"""In-process A/B of a w = 16 knob through the API call
+(jerasure_matrix_encode, RS(10,4) w = 16, 64 MiB shards) on two shard
+layouts: separately allocated tensors (what a caller passing malloc'd shards
+gets) and the library's skewed stripe slab.  Default: the packed nibble
+kernel's grid cap (ECGPU_WIDE16_BPCU 0 / 3 / 4); --knob ECGPU_WIDE16_UNITS
+--values 0,1 compares its unit-structure form.  The knob is switched with
+ecgpu_set_knob between launches.  Run under rocprofv3 --kernel-trace;
+launches are attributed by order (rounds x layouts x settings x reps).
 
-    rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ab16 -o run -- python3 tools/ab_wide16.py
-    python3 tools/ab_wide16.py --summarize gpurun_out/ab16
+    rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ab16 -o run -- python3 tools/ab_wide16.py [--knob K --values a,b]
+    python3 tools/ab_wide16.py --summarize gpurun_out/ab16 [--knob K --values a,b]
 """
 from __future__ import annotations
 
@@ -19,6 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+KNOB = "ECGPU_WIDE16_BPCU"
 SETTINGS = ["0", "3", "4"]
 LAYOUTS = ["separate", "slab"]
 ROUNDS, REPS = 6, 5
@@ -40,7 +44,7 @@ def run():
         for L in LAYOUTS:
             d, c = lay[L]
             for st in SETTINGS:
-                N.set_knob("ECGPU_WIDE16_BPCU", int(st))
+                N.set_knob(KNOB, int(st))
                 for _ in range(REPS):
                     E.jerasure.jerasure_matrix_encode(k, m, w, M, d, c, S)
     torch.cuda.synchronize()
@@ -55,16 +59,20 @@ def summarize(d):
     for _ in range(ROUNDS):
         for L in LAYOUTS:
             for st in SETTINGS:
-                out.setdefault(f"{L} bpcu={st}", []).extend(durs[i:i + REPS])
+                out.setdefault(f"{L} {KNOB}={st}", []).extend(durs[i:i + REPS])
                 i += REPS
     res = {key: {"median_us": round(statistics.median(v), 1), "min_us": round(min(v), 1), "n": len(v)}
            for key, v in out.items()}
-    print(json.dumps({"kernel": "gf_apply_wide_nib16<4>, RS(10,4) w=16 64 MiB encode", "launches": len(durs),
-                      "results": res}, indent=1))
+    names = sorted({r["Kernel_Name"].split("(")[0] for r in rows})
+    print(json.dumps({"kernel": names, "call": "jerasure_matrix_encode RS(10,4) w=16 64 MiB", "knob": KNOB,
+                      "launches": len(durs), "results": res}, indent=1))
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--summarize")
+    ap.add_argument("--knob", default=KNOB)
+    ap.add_argument("--values", default=",".join(SETTINGS))
     a = ap.parse_args()
+    KNOB, SETTINGS = a.knob, a.values.split(",")
     summarize(a.summarize) if a.summarize else run()

@@ -1451,8 +1451,9 @@ struct WidePipeShape {
   static constexpr int CH = (K + NCH - 1) / NCH;
 };
 
-template <int K, int R, int MODE, int WPE = 1, int NCHO = 0>
+template <int K, int R, int MODE, int WPE = 1, int NCHO = 0, int FG = 4>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_apply_wide_pipe(ApplyArgs a) {
+  static_assert(FG == 4 || FG == 2, "lookups folded four or two at a time");
   constexpr bool W16 = MODE == kPipeW16;
   constexpr int U = MODE == kPipeW32Unit ? 1 : 0;
   static_assert(U == 0 || R >= 2, "the unit form needs a row besides the unit row");
@@ -1525,11 +1526,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         const uint32_t xv = x[u][cc];
         const uint32_t ns[2] = {(xv << kSh) & kNibMask, (xv >> (4 - kSh)) & kNibMask};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {  // lookups in two groups of four, each folded before the next
+        for (int h = 0; h < 8 / FG; ++h) {  // lookups in groups of FG, each folded before the next
           uint32_t v[4][EW];
 #pragma unroll
-          for (int tt = 0; tt < 4; ++tt) {
-            const int t = h * 4 + tt;
+          for (int tt = 0; tt < FG; ++tt) {
+            const int t = h * FG + tt;
             const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
                                 uint32_t(t * 16 * EB);
             if constexpr (EW == 1) {
@@ -1547,13 +1548,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           if constexpr (W16) {
 #pragma unroll
             for (int q = 0; q < EW; ++q) {
-              uint32_t& e = h == 0 ? lo[cc][q] : hi[cc][q];  // tables 0-3 low word, 4-7 high word
-              e = xor3(xor3(e, v[0][q], v[1][q]), v[2][q], v[3][q]);
+              uint32_t& e = h * FG < 4 ? lo[cc][q] : hi[cc][q];  // tables 0-3 low word, 4-7 high word
+              e = FG == 4 ? xor3(xor3(e, v[0][q], v[1][q]), v[2][q], v[3][q]) : xor3(e, v[0][q], v[1][q]);
             }
           } else {
 #pragma unroll
             for (int l = 0; l < L; ++l)
-              acc[l + U][cc] = xor3(xor3(acc[l + U][cc], v[0][l], v[1][l]), v[2][l], v[3][l]);
+              acc[l + U][cc] = FG == 4 ? xor3(xor3(acc[l + U][cc], v[0][l], v[1][l]), v[2][l], v[3][l])
+                                       : xor3(acc[l + U][cc], v[0][l], v[1][l]);
           }
         }
       }

@@ -495,6 +495,20 @@ int main(int argc, char** argv) {
           vs.push_back({"pipe_wpe6", reinterpret_cast<const void*>(&gf_apply_wide_pipe<10, 4, kPipeW32Unit, 6>),
                         unsigned(nib_lds_bytes(K, 4, 1))});
         }
+        // round 4: chunkings that fit 128 VGPRs (4 workgroups per CU) at K = 12
+        // (6 or 8 chunks: 128 VGPRs; production's 4 chunks: 131, 3 per CU)
+        if (K == 12) {
+          vs.push_back({"pipe_nch6", reinterpret_cast<const void*>(&gf_apply_wide_pipe<12, 4, kPipeW32Unit, 1, 6>),
+                        unsigned(nib_lds_bytes(K, 4, 1))});
+          vs.push_back({"pipe_nch8", reinterpret_cast<const void*>(&gf_apply_wide_pipe<12, 4, kPipeW32Unit, 1, 8>),
+                        unsigned(nib_lds_bytes(K, 4, 1))});
+        }
+        if (K == 11) {
+          vs.push_back({"pipe_nch2", reinterpret_cast<const void*>(&gf_apply_wide_pipe<11, 4, kPipeW32Unit, 1, 2>),
+                        unsigned(nib_lds_bytes(K, 4, 1))});
+          vs.push_back({"pipe_nch6", reinterpret_cast<const void*>(&gf_apply_wide_pipe<11, 4, kPipeW32Unit, 1, 6>),
+                        unsigned(nib_lds_bytes(K, 4, 1))});
+        }
       }
     }
   } else {
@@ -516,6 +530,10 @@ int main(int argc, char** argv) {
         vs.push_back({b ? "prod_pipe16_grid" + std::to_string(b) : "prod_pipe16", f, l16, b});
     if (unit_rc) {
       const unsigned lu = unsigned((K - 1) * nib16_source_bytes(3));
+      // round 4: the unit form in production (gf_apply_wide_nib16<4, 1>, the wide16_units knob)
+      for (int b : {0, 3})
+        vs.push_back({std::string("prod_nib16u") + (b ? "_grid3" : ""),
+                      reinterpret_cast<const void*>(&gf_apply_wide_nib16<4, 1>), lu, b});
       for (int b : {0, 2, 3, 4}) {
         const std::string gs = b ? "_grid" + std::to_string(b) : "";
         vs.push_back({"n16u_c8_g1" + gs, reinterpret_cast<const void*>(&lab::nib16u<4, 8, 1>), lu, b});

@@ -470,14 +470,16 @@ int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
     // K, the next chunk's loads in flight during this chunk's lookups) for
     // launches of whole 256-column blocks, where it measured faster: the
     // w = 32 unit form with K = 7..10 sources (RS(K,4) 64 MiB, in one process:
-    // K = 7 148 -> 139 us, 8 162 -> 149, 10 197 -> 191; K = 5, 11, 12 equal or
+    // K = 7 148 -> 139 us, 8 162 -> 149, 10 197 -> 191; K = 5, 11 equal or
     // slower, and so were the general w = 32 and the w = 16 forms outside
-    // K = 10 -- profiles/r03_wide_lab.jsonl, "r03 pipe K sweep").
+    // K = 10 -- profiles/r03_wide_lab.jsonl, "r03 pipe K sweep") and, since
+    // round 4, K = 12 in six chunks (227.6 -> 216.8 us,
+    // profiles/r04_wide_lab_k12.jsonl; K = 11 stays level, 210.9 vs 211.0).
     // ECGPU_WIDE_PIPE: 1 that rule (default), 0 never, 2 every whole-block
     // launch of every mode (tests, A/B).
     const int pipe = knob(Knob::kWidePipe);
     // (the pipelined w = 16 form has no unit structure: it packs every row)
-    const bool pipe_shape = pipe == 2 || (pipe == 1 && !pack16 && unit_rc && K >= 7 && K <= 10);
+    const bool pipe_shape = pipe == 2 || (pipe == 1 && !pack16 && unit_rc && ((K >= 7 && K <= 10) || K == 12));
     bool piped = false;
     if (nib && nvec > 0 && nvec % dev::kBlock == 0 && pipe_shape)
       if (KernelFn f = wide_pipe_kernel(K, R, pack16 ? dev::kPipeW16 : unit_rc ? dev::kPipeW32Unit : dev::kPipeW32)) {

@@ -1325,7 +1325,10 @@ __host__ __device__ constexpr int nib16_source_bytes(int R) { return kNibWords *
 // the sources and source 0 is XORed into every row, so the LDS holds the
 // packed pairs of rows 1..R-1 (pair p = rows 1 + 2p, 2 + 2p) for sources
 // 1..K-1 only -- 1/K fewer lookups, and for R = 3 one dword entry instead of
-// two.  Selected by the wide16_units knob (ECGPU_WIDE16_UNITS).
+// two.  Production for such launches since round 4 (the wide16_units knob,
+// ECGPU_WIDE16_UNITS; RS(10,4) 64 MiB through jerasure_matrix_encode 176.0 ->
+// 174.7 us on separate shards, 174.1 -> 171.1 on the slab, lab 171.0 -> 168.9,
+// profiles/r04_ab_wide16_units.json, r04_wide_lab_w16.jsonl).
 template <int R, int U = 0>
 __global__ __launch_bounds__(kBlock) void gf_apply_wide_nib16(ApplyArgs a) {
   static_assert(U == 0 || R >= 2, "the unit form needs a row besides the unit row");
@@ -1445,9 +1448,15 @@ enum WidePipeMode : int { kPipeW32 = 0, kPipeW32Unit = 1, kPipeW16 = 2 };
 template <int K, int MODE, int NCHO = 0>
 struct WidePipeShape {
   // chunks per column: w = 32 four for K = 7..12 (RS(10,4): 3 + 3 + 3 + 1,
-  // 101 VGPRs, 4 workgroups per CU), w = 16 two (5 + 5); NCHO > 0 overrides
-  // (even)
-  static constexpr int NCH = NCHO > 0 ? NCHO : MODE == kPipeW16 ? 2 : 2 * ((K + 5) / 6);
+  // 101 VGPRs, 4 workgroups per CU) except the unit form at K = 12: six
+  // chunks of 2 hold 128 VGPRs (4 workgroups per CU) where four hold 131 (3
+  // per CU) -- RS(12,4) w = 32 64 MiB 235.3 -> 216.8 us, and 4.7 % under the
+  // unpipelined unit kernel's 227.6 (tools/wide_lab.hip, round 4); w = 16
+  // two (5 + 5); NCHO > 0 overrides (even)
+  static constexpr int NCH = NCHO > 0                             ? NCHO
+                             : MODE == kPipeW16                   ? 2
+                             : (MODE == kPipeW32Unit && K == 12) ? 6
+                                                                  : 2 * ((K + 5) / 6);
   static constexpr int CH = (K + NCH - 1) / NCH;
 };
 

@@ -35,7 +35,7 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_WIDE_UNITS", "wide_units", 1},
     {"ECGPU_WIDE_PIPE", "wide_pipe", 1},
     {"ECGPU_WIDE16_BPCU", "wide16_bpcu", 3},
-    {"ECGPU_WIDE16_UNITS", "wide16_units", 0},
+    {"ECGPU_WIDE16_UNITS", "wide16_units", 1},
     {"ECGPU_DEVICE", "device", -1},
     {"ECGPU_BOUNCE_KIB", "bounce_kib", 2048},
     {"ECGPU_ZC_KIB", "zc_kib", 1024},

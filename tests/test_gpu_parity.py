@@ -1006,7 +1006,7 @@ _PIPE_SHAPES = [(1, 1), (2, 2), (3, 4), (4, 1), (5, 3), (6, 4), (7, 2), (8, 3), 
 
 # every shape at 3 column blocks; the column loop run many times (1600
 # blocks) on three shapes -- explicit lists, so no test ID exists only to skip
-_PIPE_CASES = [(k, m, 3) for k, m in _PIPE_SHAPES] + [(k, m, 1600) for k, m in ((10, 4), (16, 4), (5, 3))]
+_PIPE_CASES = [(k, m, 3) for k, m in _PIPE_SHAPES] + [(k, m, 1600) for k, m in ((10, 4), (12, 4), (16, 4), (5, 3))]
 
 
 @pytest.mark.parametrize("w", [16, 32])

@@ -15,6 +15,10 @@ pageable numpy arrays or pinned tensors -- so every staging mode of a
 synchronous call (device, zero-copy, bounce, outputs in coherent memory,
 HIP copies, pinned in place) is crossed with every shape class.
 ECGPU_FUZZ_CASES sets the case count (default 1500, ~15 s on MI355X).
+
+test_fuzz_aliased_calls_vs_reference repeats buffers inside a call and
+shifts one onto another (the buffer contract); ECGPU_FUZZ_ALIAS_CASES
+(default 300).
 """
 import os
 
@@ -133,3 +137,123 @@ def test_fuzz_sync_calls_vs_reference(ec, gpu, reference):
             assert np.array_equal(_host([ga])[0], ra), ctx + (op, c)
             assert np.array_equal(_host([gb])[0], rb), ctx + (op, c)
     assert all(v > cases // 8 for v in kinds.values()), kinds
+
+
+def _aliased(n, rng):
+    """slot i -> the slot whose buffer it uses: itself, or (with probability
+    1/4) an earlier slot -- identical pointers, as a caller that passes one
+    buffer twice."""
+    owner = []
+    for i in range(n):
+        owner.append(int(rng.integers(0, i)) if i and rng.random() < 0.25 else i)
+    return owner
+
+
+def test_fuzz_aliased_calls_vs_reference(ec, gpu, reference):
+    """Calls whose pointer arrays repeat buffers (a coding shard that is also a
+    data shard, two outputs on one buffer, r3 == r1): the reference's
+    sequential semantics, replayed by the planner, bit-exact on device and
+    pageable buffers.  And the same calls with one buffer shifted onto
+    another by 1..size-1 bytes: rejected (EcgpuError, ECGPU_ERR_ARG) with
+    every buffer untouched (buffer_contract.hpp)."""
+    import torch
+    from erasure_coding_test_amd import _native as N
+    cases = int(os.environ.get("ECGPU_FUZZ_ALIAS_CASES", "300"))
+    rng = np.random.default_rng(4242)
+    done = {"encode": 0, "dotprod": 0, "decode": 0, "region": 0, "rejected": 0}
+    for case in range(cases):
+        kind = ("encode", "dotprod", "decode", "region")[int(rng.integers(0, 4))]
+        where = ("device", "pageable")[int(rng.integers(0, 2))]
+        size = int(rng.choice([8, 4096, 65536 + 8, 262144, (1 << 20) + 8]))
+        shift = rng.random() < 0.2
+        if kind == "region":
+            k, m = 1, 2
+        elif kind == "decode":
+            k, m = int(rng.integers(2, 11)), int(rng.integers(1, 5))
+        else:
+            k, m = int(rng.integers(1, 13)), int(rng.integers(1, 6))
+        n = k + m
+        owner = _aliased(n, rng)
+        uniq = sorted(set(owner))
+        pool = {u: rng.integers(0, 256, size, dtype=np.uint8) for u in uniq}
+        ctx = (case, kind, where, size, k, m, owner)
+
+        def call(mod, bufs):
+            d, c = bufs[:k], bufs[k:]
+            if kind == "encode":
+                M = [int(x) for x in rng_m.choice([0, 1, 2, 0x8E, 77], size=k * m)]
+                if mod is None:
+                    reference.matrix_encode(k, m, np.array(M).reshape(m, k), d, c, size)
+                else:
+                    mod.jerasure.jerasure_matrix_encode(k, m, 8, M, d, c, size)
+                return 0
+            if kind == "dotprod":
+                row = [int(x) for x in rng_m.choice([0, 1, 3, 0x1D], size=k)]
+                dest = int(rng_m.integers(0, n))
+                if mod is None:
+                    reference.matrix_dotprod(k, row, None, dest, d, c, size)
+                else:
+                    mod.jerasure.jerasure_matrix_dotprod(k, 8, row, None, dest, d, c, size)
+                return 0
+            if kind == "decode":
+                M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+                er = sorted(int(x) for x in rng_m.choice(n, size=int(rng_m.integers(1, m + 1)), replace=False))
+                if mod is None:
+                    return reference.matrix_decode(k, m, np.array(M).reshape(m, k), 0, er, d, c, size)
+                return mod.jerasure.jerasure_matrix_decode(k, m, 8, M, 0, er, d, c, size)
+            op = int(rng_m.integers(0, 3))
+            a, b, x = bufs[0], bufs[1], bufs[2]
+            if op == 0:
+                (reference.region_xor if mod is None else mod.galois.galois_region_xor)(a, b, x, size)
+            else:
+                f = reference.region_multiply if mod is None else mod.galois.galois_w08_region_multiply
+                f(a, 0x35, size, x, op - 1)
+            return 0
+
+        # the reference on numpy views of the host pool: slot i -> pool[owner[i]]
+        ref_pool = {u: v.copy() for u, v in pool.items()}
+        rng_m = np.random.default_rng(case)
+        rc_ref = call(None, [ref_pool[owner[i]] for i in range(n)])
+        if where == "device":
+            gpool = {u: torch.from_numpy(v.copy()).to(gpu) for u, v in pool.items()}
+        else:
+            gpool = {u: v.copy() for u, v in pool.items()}
+        if shift:
+            # one slot (read or written) moved onto a written slot's buffer by s bytes
+            big = {u: (torch.zeros(2 * size, dtype=torch.uint8, device=gpu) if where == "device"
+                       else np.zeros(2 * size, np.uint8)) for u in uniq}
+            for u in uniq:
+                big[u][:size] = gpool[u]
+            s = int(rng.integers(1, size)) if size > 1 else 1
+            victim, target = int(rng.integers(0, n)), int(rng.integers(k, n))
+            if owner[victim] == owner[target]:
+                continue
+            bufs = [big[owner[i]][:size] for i in range(n)]
+            bufs[victim] = big[owner[target]][s:s + size]
+            before = {u: (big[u].cpu().numpy().copy() if where == "device" else big[u].copy()) for u in uniq}
+            rng_m = np.random.default_rng(case)
+            try:
+                call(ec, bufs)
+                raised = False
+            except N.EcgpuError as ex:
+                assert "identical or disjoint" in str(ex), ctx + (str(ex),)
+                raised = True
+            # an output may not be written (all-zero dotprod row, decode with no erasure to fill,
+            # a coefficient-0 region op): the call then has no written region and may run
+            if not raised:
+                continue
+            done["rejected"] += 1
+            torch.cuda.synchronize()
+            for u in uniq:
+                now = big[u].cpu().numpy() if where == "device" else big[u]
+                assert np.array_equal(now, before[u]), ctx + ("touched after rejection", u)
+            continue
+        rng_m = np.random.default_rng(case)
+        rc = call(ec, [gpool[owner[i]] for i in range(n)])
+        torch.cuda.synchronize()
+        assert rc == rc_ref, ctx
+        for u in uniq:
+            got = gpool[u].cpu().numpy() if where == "device" else gpool[u]
+            assert np.array_equal(got, ref_pool[u]), ctx + (u,)
+        done[kind] += 1
+    assert all(v > 0 for v in done.values()), done

@@ -372,6 +372,7 @@ const void* pipe_fn(int K, int mode) {
     case 5: return pick(std::integral_constant<int, 5>{});
     case 7: return pick(std::integral_constant<int, 7>{});
     case 8: return pick(std::integral_constant<int, 8>{});
+    case 9: return pick(std::integral_constant<int, 9>{});
     case 10: return pick(std::integral_constant<int, 10>{});
     case 11: return pick(std::integral_constant<int, 11>{});
     case 12: return pick(std::integral_constant<int, 12>{});

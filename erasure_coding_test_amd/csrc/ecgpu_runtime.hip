@@ -103,9 +103,13 @@ hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t 
 // multiplies (decode{0,1,2,3}: 40 non-unit coefficients over 14 shards)
 // needs the occupancy to hide its VALU work and loses 7 %, so such launches
 // stay uncapped (cap_for).  The cap is an unused dynamic LDS allocation of
-// LDS_per_CU / blocks (rounded down to 512 B).  ECGPU_BLOCKS_PER_CU fixes the
-// block count (0 = never cap).
-unsigned residency_lds_bytes(int device, int streams) {
+// LDS_per_CU / blocks (rounded down to 512 B).  A kernel with static LDS of
+// its own (the LDS engine's tables) gets that much less and a further 4 KiB
+// margin, rounded down to 4 KiB: RS(10,4) at "3 per CU" with 1,280 B of
+// tables, dynamic 52,736 B (1.8 KiB spare) ran at 2 per CU's speed (989 us),
+// 40,960-49,152 B at 902-905 (tools/encode_lab.hip --lds 2).
+// ECGPU_BLOCKS_PER_CU fixes the block count (0 = never cap).
+unsigned residency_lds_bytes(int device, int streams, unsigned static_bytes = 0) {
   static std::once_flag once;
   static int per_cu = 0;
   std::call_once(once, [&] {
@@ -115,8 +119,11 @@ unsigned residency_lds_bytes(int device, int streams) {
   const int fixed = knob(Knob::kBlocksPerCu);
   const int blocks = fixed >= 0 ? fixed : (streams <= 9 ? 4 : 3);
   if (blocks <= 0 || per_cu <= 0) return 0;
-  const unsigned b = unsigned(per_cu / blocks) & ~511u;
-  return b > unsigned(per_cu / (blocks + 1)) ? b : 0u;
+  const unsigned total = unsigned(per_cu / blocks) & ~511u;
+  const unsigned reserve = static_bytes ? static_bytes + 4096u : 0u;
+  if (total <= reserve) return 0;
+  const unsigned b = (total - reserve) & (static_bytes ? ~4095u : ~511u);
+  return b + static_bytes > unsigned(per_cu / (blocks + 1)) ? b : 0u;
 }
 
 // Per-launch policy of the production kernel (A/B on MI355X in the bench's
@@ -565,8 +572,11 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
     const bool use_lds = p->kind == ECGPU_KERNEL_LDS;
     KernelFn vec_fn = spec ? spec_kernel(use_lds, K, R, unit_variant(p->coef, K, r0, R), p->nt) : generic_fn(R);
     const int vec = 1;
-    // (the LDS engine runs uncapped: capping it cost 4 % encode, 16 % decode{0})
-    const bool cap = !use_lds && cap_for(K, R, mul_terms);
+    // Both engines follow the cap rule; the LDS engine's allocation leaves room
+    // for its K * 128 B of tables (tools/encode_lab.hip --lds: RS(10,4) encode
+    // 1008 us uncapped, 902 at 3 per CU, v_perm 890).
+    const bool cap = cap_for(K, R, mul_terms);
+    const unsigned static_lds = use_lds && spec ? unsigned(K) * 32u * 4u : 0u;
     uint64_t unit = 0, zero = 0;
     if (spec)
       for (int r = 0; r < R; ++r)
@@ -597,7 +607,7 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream) {
       if (nvec > 0) {
         const int64_t per_block = int64_t(dev::kBlock) * vec;
         const dim3 grid(unsigned((nvec + per_block - 1) / per_block), unsigned(ns));
-        const unsigned lds = cap ? residency_lds_bytes(p->device, K + R) : 0u;
+        const unsigned lds = cap ? residency_lds_bytes(p->device, K + R, static_lds) : 0u;
         ECGPU_HIP(launch(vec_fn, grid, block, a, stream, lds));
       }
       if (byte0 < p->size) {

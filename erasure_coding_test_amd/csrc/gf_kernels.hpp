@@ -696,6 +696,16 @@ __device__ __forceinline__ uint32_t lds_word(lds_u8* base, uint32_t byte_off) {
 template <int K, int R>
 __global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lut[K * 32];  // [j][h][v]
+  // The column's K loads go out before the table staging and its barrier, so
+  // their HBM latency overlaps the staging (RS(10,4) encode at 3 workgroups
+  // per CU 918 -> 902 us, tools/encode_lab.hip --lds).
+  const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  const bool live = col < a.nvec;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = live ? load16t<1>(sp[j], col) : u32x4{0u, 0u, 0u, 0u};
   // entry (j, h, v): byte r = coef[r][j] * (v << 4h), from the per-coefficient
   // nibble tables ntab[r][j] = {c*v (16 B), c*(v << 4) (16 B)}
   for (int i = threadIdx.x; i < K * 32; i += kBlock) {
@@ -706,18 +716,10 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
     lut[i] = e;
   }
   __syncthreads();
-
-  const int64_t col = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (col >= a.nvec) return;
-  const int s = blockIdx.y;
-  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  if (!live) return;
   uint8_t* dp[R];  // all pointers before the first store (see gf_apply_body)
 #pragma unroll
   for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
-
-  u32x4 x[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) x[j] = load16t<1>(sp[j], col);
 
   lds_u8* lb = (lds_u8*)lut;  // C cast: generic -> LDS address space
   uint32_t e[4][4];  // [dword c][byte position b]: byte r = row r's product byte

@@ -143,17 +143,108 @@ __global__ __launch_bounds__(256) void enc_pipe(ApplyArgs a, int stripes) {
     it = nx;
   }
 }
+
+// The LDS nibble-table engine (gf_apply_lds) with the column's K source loads
+// issued BEFORE the per-workgroup table staging and its barrier, so the HBM
+// latency of the first (and only) loads overlaps the staging.
+template <int K, int R>
+__global__ __launch_bounds__(256) void lds_early(ApplyArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lut[K * 32];
+  const int64_t col = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  const bool live = col < a.nvec;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = live ? load16t<1>(sp[j], col) : u32x4{0u, 0u, 0u, 0u};
+  for (int i = threadIdx.x; i < K * 32; i += 256) {
+    const int j = i >> 5, hv = i & 31;
+    uint32_t e = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) e |= uint32_t(a.ntab[(r * K + j) * 32 + hv]) << (8 * r);
+    lut[i] = e;
+  }
+  __syncthreads();
+  if (!live) return;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  lds_u8* lb = (lds_u8*)lut;
+  uint32_t e[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) e[c][b] = 0u;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t xl = (x[j][c] & 0x0F0F0F0Fu) << 2;
+      const uint32_t xh = (x[j][c] >> 2) & 0x3C3C3C3Cu;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t sel = 0x0C0C0C00u | uint32_t(b);
+        const uint32_t lo = lds_word(lb, __builtin_amdgcn_perm(xl, xl, sel) + uint32_t(j * 128));
+        const uint32_t hi = lds_word(lb, __builtin_amdgcn_perm(xh, xh, sel) + uint32_t(j * 128 + 64));
+        e[c][b] = xor3(e[c][b], lo, hi);
+      }
+    }
+  }
+  u32x4 acc[R];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint32_t p01l = __builtin_amdgcn_perm(e[c][1], e[c][0], 0x05010400u);
+    const uint32_t p23l = __builtin_amdgcn_perm(e[c][3], e[c][2], 0x05010400u);
+    const uint32_t p01h = __builtin_amdgcn_perm(e[c][1], e[c][0], 0x07030602u);
+    const uint32_t p23h = __builtin_amdgcn_perm(e[c][3], e[c][2], 0x07030602u);
+    acc[0][c] = __builtin_amdgcn_perm(p23l, p01l, 0x05040100u);
+    if constexpr (R > 1) acc[1][c] = __builtin_amdgcn_perm(p23l, p01l, 0x07060302u);
+    if constexpr (R > 2) acc[2][c] = __builtin_amdgcn_perm(p23h, p01h, 0x05040100u);
+    if constexpr (R > 3) acc[3][c] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
+}
+
+// The production body with a workgroup barrier: WHERE 0 after the loads (the
+// compiler waits for them first -- the LDS engine's early-load form has the
+// same shape), 1 between the arithmetic and the stores, 2 after the loads
+// without waiting for them (s_barrier alone).
+template <int K, int R, int UNITS, int WHERE>
+__global__ __launch_bounds__(256) void enc_sync(ApplyArgs a) {
+  const int64_t col = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  const bool live = col < a.nvec;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = live ? load16t<1>(sp[j], col) : u32x4{0u, 0u, 0u, 0u};
+  if constexpr (WHERE == 0) __syncthreads();
+  if constexpr (WHERE == 2) __builtin_amdgcn_s_barrier();
+  u32x4 acc[R];
+  combine<K, R, UNITS, 3>(a, x, acc);
+  if constexpr (WHERE == 1) __syncthreads();
+  if (!live) return;
+#pragma unroll
+  for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
+}
 }  // namespace lab
 
 bool g_early0 = false;  // --early0 1: skew mode also times lab::enc_early0 on every slab
 bool g_vec2 = false;    // --vec2 1: ... and the production body with two columns per lane (VEC = 2)
 bool g_dense = false;   // --dense 1: a C4-like dense 4 x 10 map (no 0 / 1 coefficients) instead of the encode
+int g_lds = 0;          // --lds 1: the LDS nibble-table engine (production form and lab forms) beside the v_perm production;
+                        // --lds 2: both engines at 3 workgroups per CU under dynamic LDS allocations of several sizes
 
 struct Variant {
   std::string name;
   const void* fn;
   int bs;
   int blocks_per_cu;  // 0: uncapped
+  unsigned lds = 0;   // > 0: this dynamic LDS allocation instead of the blocks_per_cu rule
 };
 
 // builds the production 3-bit-slice tables (ecgpu_runtime.hip build_tables)
@@ -188,6 +279,9 @@ size_t window(size_t S, int shard) { return (size_t(shard) * 0x9E3779B1ull % (S 
 
 template <int k, int m>
 int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int reps);
+template <int k, int m>
+int variant_ab(int stripes, size_t S, int skew_kib, int rounds, int reps);
+int g_sync = 0;  // --sync 1: the production body with workgroup barriers (lab::enc_sync) and the LDS engine, at the library's cap
 
 int main(int argc, char** argv) {
   int stripes = 96, rounds = 7, reps = 10, kk = 10, mm = 4, kib = 4096, skew_kib = -1;
@@ -204,6 +298,8 @@ int main(int argc, char** argv) {
     else if (f == "--early0") g_early0 = std::atoi(argv[i + 1]) != 0;
     else if (f == "--vec2") g_vec2 = std::atoi(argv[i + 1]) != 0;
     else if (f == "--dense") g_dense = std::atoi(argv[i + 1]) != 0;
+    else if (f == "--lds") g_lds = std::atoi(argv[i + 1]);
+    else if (f == "--sync") g_sync = std::atoi(argv[i + 1]);
     else if (f == "--skew-kib") skew_kib = std::atoi(argv[i + 1]);
     else if (f == "--skews") {
       std::string v = argv[i + 1];
@@ -224,9 +320,17 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "skew A/B covers RS(10,4), RS(12,4), RS(6,3), RS(4,2)\n");
     return 2;
   }
-  constexpr int k = 10, m = 4;
-  // the library's stride for 4 MiB shards (shard_stride.hpp), or --skew-kib
-  const size_t S = size_t(4) << 20;
+  if (kk == 10 && mm == 4) return variant_ab<10, 4>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
+  if (kk == 6 && mm == 3) return variant_ab<6, 3>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
+  if (kk == 12 && mm == 4) return variant_ab<12, 4>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
+  std::fprintf(stderr, "variant A/B covers RS(10,4), RS(6,3), RS(12,4)\n");
+  return 2;
+}
+
+// Every variant of the selected mode on one slab of `stripes` RS(k,m) stripes
+// of S-byte shards at the library's stride (or S + skew_kib KiB).
+template <int k, int m>
+int variant_ab(int stripes, size_t S, int skew_kib, int rounds, int reps) {
   const size_t stride = skew_kib >= 0 ? S + size_t(skew_kib) * 1024 : size_t(shard_stride(int64_t(S)));
   int* M = vandermonde_coding_matrix(k, m, 8);
   if (g_dense) {
@@ -236,6 +340,14 @@ int main(int argc, char** argv) {
   std::vector<uint32_t> ptab(size_t(m) * k * kP3Words);
   for (int r = 0; r < m; ++r)
     for (int j = 0; j < k; ++j) build_p3(M[r * k + j], &ptab[(size_t(r) * k + j) * kP3Words]);
+  // the LDS engine's per-coefficient nibble tables (ecgpu_runtime.hip): c*v, then c*(v << 4)
+  std::vector<uint8_t> ntab(size_t(m) * k * 32);
+  for (int r = 0; r < m; ++r)
+    for (int j = 0; j < k; ++j)
+      for (int v = 0; v < 16; ++v) {
+        ntab[(size_t(r) * k + j) * 32 + v] = uint8_t(single_multiply(M[r * k + j], v, 8));
+        ntab[(size_t(r) * k + j) * 32 + 16 + v] = uint8_t(single_multiply(M[r * k + j], v << 4, 8));
+      }
   uint8_t* slab = nullptr;
   const size_t slab_bytes = stride * size_t(k + m) * size_t(stripes);
   CK(hipMalloc(&slab, slab_bytes));
@@ -261,8 +373,12 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(d_src, hs.data(), sizeof(void*) * hs.size(), hipMemcpyHostToDevice));
   CK(hipMemcpy(d_dst, hd.data(), sizeof(void*) * hd.size(), hipMemcpyHostToDevice));
   CK(hipMemcpy(d_ptab, ptab.data(), 4 * ptab.size(), hipMemcpyHostToDevice));
+  uint8_t* d_ntab = nullptr;
+  CK(hipMalloc(&d_ntab, ntab.size()));
+  CK(hipMemcpy(d_ntab, ntab.data(), ntab.size(), hipMemcpyHostToDevice));
   ApplyArgs a{};
   a.ptab = d_ptab;
+  a.ntab = d_ntab;
   a.src = d_src;
   a.dst = d_dst;
   a.nvec = int64_t(S / 16);
@@ -276,7 +392,36 @@ int main(int argc, char** argv) {
   a.nt = 1;
   constexpr int U = kUnitCol0 | kUnitRow0, N = kUnitNone;
   // bs < 0: the persistent pipelined form (a resident round of |bs| workgroups per CU)
-  std::vector<Variant> vs = g_dense ? std::vector<Variant>{
+  using V = Variant;
+  const void* const vperm = reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>);
+  const void* const ldsk = reinterpret_cast<const void*>(&gf_apply_lds<k, m>);
+  const int cap = k + m <= 9 ? 4 : 3;  // ecgpu_runtime.hip residency_lds_bytes
+  const unsigned lds_cap = ((unsigned(163840 / cap) & ~511u) - 128u * k - 4096u) & ~4095u;
+  std::vector<Variant> vs = g_sync ? std::vector<Variant>{
+      V{"prod", vperm, 256, cap},
+      V{"sync_after_loads", reinterpret_cast<const void*>(&lab::enc_sync<k, m, U, 0>), 256, cap},
+      V{"sync_before_stores", reinterpret_cast<const void*>(&lab::enc_sync<k, m, U, 1>), 256, cap},
+      V{"barrier_no_wait", reinterpret_cast<const void*>(&lab::enc_sync<k, m, U, 2>), 256, cap},
+      V{"lds_engine", ldsk, 256, cap, lds_cap},
+  } : g_lds == 2 ? std::vector<Variant>{
+      V{"prod_bs256_cap3", vperm, 256, 3},
+      V{"vperm_dyn41472", vperm, 256, 3, 41472},
+      V{"vperm_dyn45056", vperm, 256, 3, 45056},
+      V{"vperm_dyn49152", vperm, 256, 3, 49152},
+      V{"vperm_dyn52224", vperm, 256, 3, 52224},
+      V{"lds_dyn40960", ldsk, 256, 3, 40960},
+      V{"lds_dyn45056", ldsk, 256, 3, 45056},
+      V{"lds_dyn49152", ldsk, 256, 3, 49152},
+      V{"lds_dyn52736", ldsk, 256, 3, 52736},
+  } : g_lds ? std::vector<Variant>{
+      {"prod_bs256_cap3", reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>), 256, 3},
+      {"prod_lds", reinterpret_cast<const void*>(&gf_apply_lds<k, m>), 256, 0},
+      {"lds_cap3", reinterpret_cast<const void*>(&gf_apply_lds<k, m>), 256, 3},
+      {"lds_cap4", reinterpret_cast<const void*>(&gf_apply_lds<k, m>), 256, 4},
+      {"lds_early", reinterpret_cast<const void*>(&lab::lds_early<k, m>), 256, 0},
+      {"lds_early_cap3", reinterpret_cast<const void*>(&lab::lds_early<k, m>), 256, 3},
+      {"lds_early_cap4", reinterpret_cast<const void*>(&lab::lds_early<k, m>), 256, 4},
+  } : g_dense ? std::vector<Variant>{
       {"prod_dense_cap3", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 3},
       {"dense_cap4", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 4},
       {"dense_uncapped", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 0},
@@ -301,6 +446,7 @@ int main(int argc, char** argv) {
   CK(hipGetDevice(&dev));
   CK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
   auto lds_of = [&](const Variant& v) -> unsigned {
+    if (v.lds > 0) return v.lds;
     if (v.blocks_per_cu <= 0) return 0u;
     const unsigned b = unsigned(lds_cu / v.blocks_per_cu) & ~511u;
     return b > unsigned(lds_cu / (v.blocks_per_cu + 1)) ? b : 0u;
@@ -382,9 +528,9 @@ int main(int argc, char** argv) {
   for (size_t v = 0; v < vs.size(); ++v) {
     std::sort(t[v].begin(), t[v].end());
     const double med = t[v][t[v].size() / 2];
-    std::printf("{\"variant\": \"%s\", \"block\": %d, \"blocks_per_cu\": %d, \"stripes\": %d, \"median_us\": %.1f, "
+    std::printf("{\"variant\": \"%s\", \"block\": %d, \"blocks_per_cu\": %d, \"dyn_lds\": %u, \"stripes\": %d, \"median_us\": %.1f, "
                 "\"min_us\": %.1f, \"GBps\": %.0f, \"frac\": %.4f}\n",
-                vs[v].name.c_str(), vs[v].bs, vs[v].blocks_per_cu, stripes, med, double(t[v][0]),
+                vs[v].name.c_str(), vs[v].bs, vs[v].blocks_per_cu, lds_of(vs[v]), stripes, med, double(t[v][0]),
                 bytes / med / 1e3, bytes / med / 1e3 / 8000.0);
   }
   return 0;

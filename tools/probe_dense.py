@@ -45,6 +45,7 @@ VARIANTS = {
     "bpcu4_always": {"cap": 1, "blocks_per_cu": 4},
     "bpcu3_always": {"cap": 1, "blocks_per_cu": 3},
     "lds_engine": {"kernel": 1},
+    "lds_engine_uncapped": {"kernel": 1, "cap": 0},
 }
 
 

@@ -357,6 +357,91 @@ constexpr unsigned split_lds(int K) {
   return unsigned(K - U) * 8u * unsigned(NP * (kWide ? 256 : 128));
 }
 
+
+// w = 16 RS(K,4) unit form without the persistent loop (round 4): one (or
+// BPW) column block(s) per workgroup, compile-time K, the column's K source
+// loads issued first, then the LDS image copied in from a packed global image
+// (a.ptab: the staging loop's output, built once on the host) and the
+// barrier -- the shape that put the w = 8 LDS engine at the v_perm engine's
+// rate.  BPW > 1: the next block's loads go out before this block's lookups.
+template <int K, int BPW>
+__global__ __launch_bounds__(kBlock) void nib16_flat(ApplyArgs a) {
+  constexpr int L = 3, EW = 2, EB = 8;  // rows 1..3 in two packed pairs per entry
+  extern __shared__ __attribute__((aligned(16))) uint8_t nib_lds[];
+  const uint8_t* const* sp = a.src;
+  uint8_t* dp[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dp[r] = a.dst[a.row0 + r];
+  int64_t col = int64_t(blockIdx.x) * BPW * kBlock + threadIdx.x;
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = col < a.nvec ? load16t<1>(kload(sp, j), col) : u32x4{0u, 0u, 0u, 0u};
+  {
+    const u32x4* img = reinterpret_cast<const u32x4*>(a.ptab);
+    constexpr int n4 = (K - 1) * kNibWords * EW / 4;
+    for (int i = threadIdx.x; i < n4; i += kBlock) reinterpret_cast<u32x4*>(nib_lds)[i] = img[i];
+  }
+  __syncthreads();
+  const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(static_cast<void*>(nib_lds)));
+#pragma unroll
+  for (int q = 0; q < BPW; ++q) {
+    u32x4 xn[K];
+    const int64_t ncol = col + kBlock;
+    if (q + 1 < BPW) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) xn[j] = ncol < a.nvec ? load16t<1>(kload(sp, j), ncol) : u32x4{0u, 0u, 0u, 0u};
+    }
+    uint32_t lo[4][EW], hi[4][EW];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < EW; ++e) lo[c][e] = hi[c][e] = 0u;
+    u32x4 row0 = x[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+      row0 ^= x[j];
+      const uint32_t jbase = lds_base + uint32_t(j - 1) * uint32_t(nib16_source_bytes(L));
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t xv = x[j][c];
+        constexpr int kSh = 3;
+        constexpr uint32_t kNibMask = 0x0F0F0F0Fu << kSh;
+        const uint32_t ns[2] = {(xv << kSh) & kNibMask, (xv >> (4 - kSh)) & kNibMask};
+        uint32_t v[8][EW];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const uint32_t ad = __builtin_amdgcn_perm(jbase, ns[t & 1], 0x0C060500u | uint32_t(t >> 1)) +
+                              uint32_t(t * 16 * EB);
+          const u32x2 qv = *(lds_u32x2*)(size_t(ad));
+          v[t][0] = qv.x;
+          v[t][1] = qv.y;
+        }
+#pragma unroll
+        for (int e = 0; e < EW; ++e) {
+          lo[c][e] = xor3(xor3(lo[c][e], v[0][e], v[1][e]), v[2][e], v[3][e]);
+          hi[c][e] = xor3(xor3(hi[c][e], v[4][e], v[5][e]), v[6][e], v[7][e]);
+        }
+      }
+    }
+    if (col < a.nvec) {
+      store16t<1>(dp[0], col, row0);
+#pragma unroll
+      for (int r = 1; r < 4; ++r) {
+        const int l = r - 1;
+        u32x4 o;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          o[c] = __builtin_amdgcn_perm(hi[c][l >> 1], lo[c][l >> 1], (l & 1) ? 0x07060302u : 0x05040100u) ^ x[0][c];
+        store16t<1>(dp[r], col, o);
+      }
+    }
+    if (q + 1 < BPW) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) x[j] = xn[j];
+    }
+    col = ncol;
+  }
+}
 }  // namespace lab
 
 // production's pipelined wide kernel (gf_apply_wide_pipe<K, 4, mode>) for the
@@ -385,6 +470,7 @@ struct Variant {
   const void* fn;
   unsigned lds;
   int bpcu = 0;  // > 0: grid of bpcu workgroups per CU (fewer resident than the occupancy allows)
+  int flat = 0;  // > 0: a non-persistent grid of one workgroup per `flat` column blocks
 };
 
 int main(int argc, char** argv) {
@@ -449,7 +535,27 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_wtab, wtab.size() * 4));
   CK(hipMemcpy(d_wtab, wtab.data(), wtab.size() * 4, hipMemcpyHostToDevice));
 
+  // the w = 16 unit form's LDS image (gf_apply_wide_nib16<4, 1>'s staging
+  // loop, done once here): dword ((j - 1) * kNibWords + e) * 2 + pr = rows
+  // 1 + 2pr | 2 + 2pr of source j's table entry e, low or high word
+  std::vector<uint32_t> img16(size_t(K > 1 ? K - 1 : 0) * kNibWords * 2);
+  for (int j = 1; j < K && w == 16; ++j)
+    for (int e = 0; e < kNibWords; ++e)
+      for (int pr = 0; pr < 2; ++pr) {
+        const bool high = (e >> 4) >= 4;
+        auto word = [&](int r) -> uint32_t {
+          if (r >= R) return 0u;
+          const uint32_t v = wtab[size_t(r * K + j) * kNibWords + e];
+          return high ? (v >> 16) : (v & 0xFFFFu);
+        };
+        img16[(size_t(j - 1) * kNibWords + e) * 2 + pr] = word(1 + 2 * pr) | (word(2 + 2 * pr) << 16);
+      }
+  uint32_t* d_img16 = nullptr;
+  CK(hipMalloc(&d_img16, std::max<size_t>(16, img16.size() * 4)));
+  if (!img16.empty()) CK(hipMemcpy(d_img16, img16.data(), img16.size() * 4, hipMemcpyHostToDevice));
+
   ApplyArgs a{};
+  a.ptab = d_img16;
   a.src = d_ptrs;
   a.dst = d_ptrs + K;
   a.nvec = int64_t(S / 16);
@@ -535,6 +641,15 @@ int main(int argc, char** argv) {
       for (int b : {0, 3})
         vs.push_back({std::string("prod_nib16u") + (b ? "_grid3" : ""),
                       reinterpret_cast<const void*>(&gf_apply_wide_nib16<4, 1>), lu, b});
+      // round 4: non-persistent forms (lab::nib16_flat), dynamic LDS sized for 2 / 3 / 4 workgroups per CU
+      if (K == 10) {
+        for (int per_cu : {2, 3, 4}) {
+          const unsigned dyn = std::max(lu, (unsigned(163840 / per_cu) & ~4095u) - 4096u);
+          const std::string ps = "_cu" + std::to_string(per_cu);
+          vs.push_back({"flat1" + ps, reinterpret_cast<const void*>(&lab::nib16_flat<10, 1>), dyn, 0, 1});
+          vs.push_back({"flat2" + ps, reinterpret_cast<const void*>(&lab::nib16_flat<10, 2>), dyn, 0, 2});
+        }
+      }
       for (int b : {0, 2, 3, 4}) {
         const std::string gs = b ? "_grid" + std::to_string(b) : "";
         vs.push_back({"n16u_c8_g1" + gs, reinterpret_cast<const void*>(&lab::nib16u<4, 8, 1>), lu, b});
@@ -554,7 +669,9 @@ int main(int argc, char** argv) {
   };
   auto launch = [&](const Variant& v, ApplyArgs args) {
     void* kargs[] = {&args};
-    CK(hipLaunchKernel(v.fn, dim3(unsigned(grid_of(v)), 1), dim3(kBlock), kargs, v.lds, nullptr));
+    const int64_t nblk = (args.nvec + kBlock - 1) / kBlock;
+    const unsigned grid = v.flat > 0 ? unsigned((nblk + v.flat - 1) / v.flat) : unsigned(grid_of(v));
+    CK(hipLaunchKernel(v.fn, dim3(grid, 1), dim3(kBlock), kargs, v.lds, nullptr));
   };
   // reference outputs from the production kernel, then a host spot check
   launch(vs[0], a);

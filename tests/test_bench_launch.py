@@ -58,7 +58,7 @@ def _env():
     return env
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])  # 8: the driver's scaling run
 def test_spawn_selftest_end_to_end(world):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--spawn-selftest"],
                        capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)

@@ -318,9 +318,9 @@ def cpu_baseline(seconds: float, host_stripe, k, m, erasures, threads: int = 1, 
     our C restatement (oracle/ec_oracle.c).  Bounded sample of the same
     workload: ONE stripe of the GPU slab (copied to the host), encode (+ the
     step's decode), repeated until `seconds` of wall time.  With threads > 1
-    each call is split by byte range over threads exactly like the reference
-    client's encode_mul_thread (client_main.cpp:1074-1164; thread 0 takes the
-    remainder); each thread is pinned to its own CPU (sched_setaffinity) and
+    each call is split by byte range over threads like the reference client's
+    encode_mul_thread (client_main.cpp:1074-1164), in whole 8-B words with the
+    remainder in the last range (the client gives it to thread 0); each thread is pinned to its own CPU (sched_setaffinity) and
     ctypes releases the GIL, so the threads run in parallel.
 
     Also the checker: the CPU's parity (and rebuilt shard) on that stripe must
@@ -346,11 +346,13 @@ def cpu_baseline(seconds: float, host_stripe, k, m, erasures, threads: int = 1, 
     coding = alloc_shards(m, S)
     cpus = host_cpus() if cpus is None else cpus
     threads = max(1, min(threads, len(cpus)))
-    ranges, off = [], 0
-    for t in range(threads):
-        n = S // threads + (S % threads if t == 0 else 0)
-        ranges.append((off, n))
-        off += n
+    # Every range but the last is a whole number of 8-B words, the last taking
+    # the remainder: the reference's add / XOR loops run in 8-B words and write
+    # up to 7 B past a range that is not (galois.cpp:452-465, :731-754), which
+    # with the client's split (thread 0 takes the remainder; e.g. 4 MiB over 96
+    # threads) lands in the next thread's range while that thread XORs into it.
+    per = (S // threads) // 8 * 8
+    ranges = [(t * per, per if t < threads - 1 else S - per * (threads - 1)) for t in range(threads)]
 
     def views(bufs, off, n):
         return [np.frombuffer((ctypes.c_uint8 * (n + 16)).from_address(b.ctypes.data + off), dtype=np.uint8)

@@ -132,3 +132,32 @@ def test_cgroup_cpu_quota(tmp_path):
     assert bench.cgroup_cpu_quota(str(tmp_path)) == 8
     assert 1 <= len(bench.host_cpus()) <= bench.HOST_THREAD_CAP
     assert len(bench.all_host_cpus()) >= len(bench.host_cpus())
+
+
+@pytest.mark.parametrize("threads", [1, 7])
+def test_cpu_baseline_thread_split_keeps_parity(threads):
+    """The multi-thread CPU baseline splits a stripe by byte range like the
+    reference client, in whole 8-B words: 7 x 599,193 + 3 B over 7 threads is
+    not, and the reference's word loops would otherwise write up to 7 B into
+    the next thread's range while that thread runs (the baseline's parity
+    check catches that)."""
+    import numpy as np
+
+    from oracle.oracle import Reference, Restatement, alloc_shards
+    try:
+        o = Reference()
+    except (FileNotFoundError, OSError):
+        o = Restatement()
+    k, m, S = 10, 4, 7 * 599193 + 3
+    rng = np.random.default_rng(5)
+    data = alloc_shards(k, S)
+    for d in data:
+        d[:S] = rng.integers(0, 256, S, dtype=np.uint8)
+    coding = alloc_shards(m, S)
+    o.matrix_encode(k, m, o.vandermonde_coding_matrix(k, m), data, coding, S)
+    stripe = np.stack([d[:S] for d in data] + [c[:S] for c in coding])
+    cpus = sorted(os.sched_getaffinity(0))
+    cpus = (cpus * threads)[:threads]
+    for _ in range(3):
+        base, ok = bench.cpu_baseline(0.2, stripe, k, m, [0], threads=threads, cpus=cpus)
+        assert ok and base["cores"] == threads

@@ -755,6 +755,53 @@ def selftest_main(args):
     return 0 if devices_ok else 1
 
 
+def sharded_c5(E, N, dev, stream, kind, nt, rank, world, per_rank=24, launches=10):
+    """BASELINE config 5 as a whole job: RS(12,4) encode of 16 MiB shards,
+    `per_rank` stripes on every rank (global stripe ids round-robin, no
+    collective), `launches` launches per rank bracketed by a barrier and a
+    device sync on both sides, the slowest rank's time.  Every rank checks its
+    first stripe against the other multiply engine.  Collective: every rank
+    calls it.  Returns the entry (the same on every rank)."""
+    import torch
+    k, m, S = 12, 4, 16 << 20
+    M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    slab, shards = E.alloc_stripes(per_rank, k, m, S, dev)
+    fill_random(slab, global_stripe_ids(per_rank, rank, world), 5)
+    p = E.encode_plan(k, m, M, dev.index).bind([st[:k] for st in shards], [st[k:] for st in shards], S)
+    p.set_kernel(kind, nt)
+    for _ in range(3):
+        p.launch(stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        p.launch(stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    barrier(world)
+    t = max_over_ranks(elapsed, world)
+    chk = torch.empty((m, S), dtype=torch.uint8, device=dev)
+    ref = E.encode_plan(k, m, M, dev.index).bind([shards[0][:k]], [[chk[i] for i in range(m)]], S)
+    ref.set_kernel(N.KERNEL_LDS if kind == N.KERNEL_PERM else N.KERNEL_PERM, True)
+    ref.launch(stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    bad = 0.0 if all(bool(torch.equal(chk[i], shards[0][k + i])) for i in range(m)) else 1.0
+    bad = max_over_ranks(bad, world)
+    p.close()
+    ref.close()
+    del slab, shards, chk
+    torch.cuda.empty_cache()
+    per_gpu_bytes = (k + m) * S * per_rank * launches
+    return {"workload": f"RS(12,4) encode, 16 MiB shards, {per_rank} stripes per GPU x {world} GPU(s), global "
+                        "stripe ids round-robin, no collective (BASELINE config 5)",
+            "n_gpus": world, "launches": launches, "ms_per_launch": round(t / launches * 1e3, 4),
+            "data_GiBps": round(world * k * S * per_rank * launches / t / 2**30, 1),
+            "hbm_frac_per_gpu": round(per_gpu_bytes / t / 1e9 / HBM_PEAK_GBS, 4),
+            "timing": "host clock between barriers, slowest rank (includes launch gaps)",
+            "parity_ok": bad == 0.0}
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -883,6 +930,9 @@ def main(argv=None):
         slab = None
         torch.cuda.empty_cache()
         configs = config_block(E, N, dev, stream, kind, bool(args.nt), main_entries)
+    c5 = None
+    if not args.no_configs and args.config == "C3":
+        c5 = sharded_c5(E, N, dev, stream, kind, bool(args.nt), rank, world)
 
     enc_frac = enc_bytes / (enc_ms / 1e3) / 1e9 / HBM_PEAK_GBS
     mine = {"rank": rank, "device": local, **device_identity(N, local), "elapsed_s": round(elapsed, 6),
@@ -897,7 +947,7 @@ def main(argv=None):
         mine["configs"] = {name: {"median_launch_ms": e["median_launch_ms"], "frac": e["frac"]}
                            for name, e in configs.items()}
     per_rank = gather(mine, world)
-    ok = all(p["parity_ok"] for p in per_rank)
+    ok = all(p["parity_ok"] for p in per_rank) and (c5 is None or c5["parity_ok"])
     devices_ok, devices_note = distinct_devices(per_rank, rehearsal)
     barrier(world)  # every rank's GPU work is done: the CPU baseline below runs alone
 
@@ -972,6 +1022,7 @@ def main(argv=None):
                               if dec_ms is not None else None),
             "per_rank": per_rank,
             "configs": configs,
+            "c5_sharded": c5,
             "cpu_baseline": cpu,
             "cpu_baseline_per_gpu_share": cpu_share,
             "cpu_baseline_all_cores": cpu_all,

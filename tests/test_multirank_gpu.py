@@ -183,6 +183,9 @@ def test_bench_gpus2_rehearsal_spawns_two_ranks(gpu):
     assert all(b and b.count(":") == 2 for b in buses) and buses[0] == buses[1], buses
     assert d["distinct_devices_ok"] is True and "rehearsal" in d["distinct_devices"]
     assert d["cpu_baseline_per_gpu_share"]["cores"] >= 1 and d["cpu_baseline_all_cores"]["cores"] >= 1
+    # BASELINE config 5 as a whole job over both ranks (barrier-bracketed, slowest rank)
+    c5 = d["c5_sharded"]
+    assert c5["n_gpus"] == 2 and c5["parity_ok"] is True and c5["data_GiBps"] > 0 and c5["hbm_frac_per_gpu"] > 0
 
 
 def test_bench_gpus_beyond_visible_devices_fails(gpu):

@@ -727,8 +727,20 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int b = 0; b < 4; ++b) e[c][b] = 0u;
+  u32x4 ux = u32x4{0u, 0u, 0u, 0u};  // XOR of the sources whose every row coefficient is 1
 #pragma unroll
   for (int j = 0; j < K; ++j) {
+    // a source that is a unit (or zero) in every row of the launch needs no
+    // lookup: wave-uniform branches on the host's masks (decode{0} is all
+    // XOR; every Vandermonde encode has column 0 all ones)
+    uint64_t colbits = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) colbits |= uint64_t(1) << (r * K + j);
+    if ((a.zero_mask & colbits) == colbits) continue;
+    if ((a.unit_mask & colbits) == colbits) {
+      ux ^= x[j];
+      continue;
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const uint32_t xl = (x[j][c] & 0x0F0F0F0Fu) << 2;  // lo nibble * 4 per byte
@@ -757,7 +769,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lds(ApplyArgs a) {
     if constexpr (R > 3) acc[3][c] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
+  for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r] ^ ux);
 }
 
 // ------------------------------------------- generic K (> kMaxSpecK) ----

@@ -263,7 +263,8 @@ def test_host_region_ops_aliasing(ec, gpu, restatement, size):
     assert np.array_equal(a[size:], a0[size:]) and np.array_equal(b[size:], b0[size:])  # padding untouched
 
 
-def test_decode_plan_batch_matches_jerasure(ec, gpu):
+@pytest.mark.parametrize("kind", [0, 1])  # v_perm engine, LDS nibble-table engine
+def test_decode_plan_batch_matches_jerasure(ec, gpu, kind):
     import torch
     k, m, size, stripes = 10, 4, 1 << 18, 4
     M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
@@ -275,12 +276,12 @@ def test_decode_plan_batch_matches_jerasure(ec, gpu):
         ec.jerasure.jerasure_matrix_encode(k, m, 8, M, d, c, size)
         shards.append(d + c)
     orig = [[t.clone() for t in st] for st in shards]
-    for er in ([0], [0, 1, 2, 3], [2, 11], [10, 11, 12, 13]):
+    for er in ([0], [0, 1, 2, 3], [2, 11], [10, 11, 12, 13], [12], [5]):
         for st in shards:
             for e in er:
                 st[e].zero_()
         dp = ec.plan.DecodePlan(k, m, M, er)
-        dp.bind_stripes(shards, size).launch()
+        dp.bind_stripes(shards, size).set_kernel(kind, True).launch()
         torch.cuda.synchronize()
         for st, o in zip(shards, orig):
             for a, b in zip(st, o):

@@ -1157,17 +1157,11 @@ int exec_staged(Ctx* c, const FusedOp& op, CallMap& m, bool inl) {
   return ECGPU_OK;
 }
 
-// Runs a fused op synchronously over `size` bytes of every buffer: maps the
-// buffers, then the cheapest staging mode for the host ones (§8 of DESIGN.md;
-// the thresholds are measured, see bounce_max / zc_max / zc_out_max).
-int execute(const FusedOp& op, int64_t size, const char* call) {
-  if (op.w != 8 && size % (op.w / 8) != 0)
-    return fail(ECGPU_ERR_ARG, "w = " + std::to_string(op.w) + ": size must be a multiple of the word size");
-  // identical or disjoint buffers, checked before anything touches the GPU
-  if (int rc = check_op_buffers(call, op, size)) return rc;
-  add_stats(op);
-  if (op.dsts.empty() || size <= 0) return ECGPU_OK;
-  const int device = current_device();
+// Runs a fused op synchronously over `size` bytes of every buffer on
+// `device`: maps the buffers, then the cheapest staging mode for the host
+// ones (§8 of DESIGN.md; the thresholds are measured, see bounce_max / zc_max
+// / zc_out_max).
+int execute_on(const FusedOp& op, int64_t size, int device) {
   CtxLease lease(device);
   if (!lease.c) return lease.rc;
   Ctx* c = lease.c;
@@ -1182,6 +1176,96 @@ int execute(const FusedOp& op, int64_t size, const char* call) {
     if (done) return ECGPU_OK;
   }
   return exec_staged(c, op, m, inl);
+}
+
+// ------------------------------------------------------- split calls ----
+// A synchronous call on host memory can be cut into contiguous 16-B-aligned
+// byte ranges that run concurrently, each on its own context (thread, stream,
+// staging) and device.  Every byte column of a fused op is independent -- a
+// column's outputs depend on that column of the sources only, identical
+// buffers included -- so the ranges' bytes are the call's.  This is the
+// reference client's own split (encode_mul_thread, client_main.cpp:1074-1164)
+// done inside one call, and SURVEY §8e's "one huge stripe: contiguous byte
+// ranges of S/N" over the visible GPUs: each range crosses its own PCIe link.
+// ECGPU_SPLIT: 0 off (default), -1 one range per visible device, N > 0 N
+// ranges over the devices in turn (N > 1 on one GPU: N contexts on it);
+// ranges are at least ECGPU_SPLIT_MIN_KIB.  Calls with a device buffer stay
+// whole (the buffer fixes the device).
+int split_ways(const FusedOp& op, int64_t size, int* ndev) {
+  const int v = knob(Knob::kSplit);
+  if (v == 0) return 1;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  *ndev = n;
+  const int64_t min_bytes = int64_t(std::max(16, knob(Knob::kSplitMinKib))) << 10;
+  const int ways = int(std::min<int64_t>(v < 0 ? n : v, size / min_bytes));
+  if (ways <= 1) return 1;
+  auto on_host = [](const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return true;  // unregistered pageable memory
+    }
+    return attr.type != hipMemoryTypeDevice && attr.type != hipMemoryTypeManaged;
+  };
+  for (void* p : op.srcs)
+    if (!on_host(p)) return 1;
+  for (void* p : op.dsts)
+    if (!on_host(p)) return 1;
+  return ways;
+}
+
+FusedOp shifted(const FusedOp& op, int64_t off) {
+  FusedOp s;
+  for (void* p : op.srcs) s.srcs.push_back(static_cast<char*>(p) + off);
+  for (void* p : op.dsts) s.dsts.push_back(static_cast<char*>(p) + off);
+  s.coef = op.coef;
+  s.w = op.w;
+  s.dst_is_src = op.dst_is_src;
+  return s;
+}
+
+int execute_split(const FusedOp& op, int64_t size, int ways, int ndev) {
+  const int64_t per = (size / ways) & ~int64_t(15);  // whole words at w = 16 / 32
+  const int first = current_device();
+  std::vector<int> rc(size_t(ways), ECGPU_OK);
+  std::vector<std::string> msg(static_cast<size_t>(ways));
+  auto run = [&](int i) {
+    const int64_t off = per * i, len = i + 1 < ways ? per : size - off;
+    rc[size_t(i)] = execute_on(shifted(op, off), len, (first + i) % ndev);
+    if (rc[size_t(i)]) msg[size_t(i)] = t_err;
+  };
+  std::vector<std::thread> workers;
+  int next = 1;
+  try {
+    for (; next < ways; ++next) workers.emplace_back(run, next);
+  } catch (const std::system_error&) {  // no thread: the rest run here, in turn
+  }
+  run(0);
+  for (int i = next; i < ways; ++i) run(i);
+  for (auto& t : workers) t.join();
+  for (int i = 0; i < ways; ++i)
+    if (rc[size_t(i)])
+      return fail(rc[size_t(i)], msg[size_t(i)] + " (byte range " + std::to_string(per * i) + " of a call split " +
+                                     std::to_string(ways) + " ways)");
+  return ECGPU_OK;
+}
+
+// A synchronous call over `size` bytes of every buffer of the fused op.
+int execute(const FusedOp& op, int64_t size, const char* call) {
+  if (op.w != 8 && size % (op.w / 8) != 0)
+    return fail(ECGPU_ERR_ARG, "w = " + std::to_string(op.w) + ": size must be a multiple of the word size");
+  // identical or disjoint buffers, checked before anything touches the GPU
+  if (int rc = check_op_buffers(call, op, size)) return rc;
+  add_stats(op);
+  if (op.dsts.empty() || size <= 0) return ECGPU_OK;
+  int ndev = 1;
+  const int ways = split_ways(op, size, &ndev);
+  if (ways > 1) return execute_split(op, size, ways, ndev);
+  return execute_on(op, size, current_device());
 }
 
 ECGPU_RT_END

@@ -48,6 +48,8 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_PIPE_D2H_WORKER", "pipe_d2h_worker", 1},
     {"ECGPU_PACKET", "packet", 0},
     {"ECGPU_SHARD_SKEW_KIB", "shard_skew_kib", -1},
+    {"ECGPU_SPLIT", "split", 0},
+    {"ECGPU_SPLIT_MIN_KIB", "split_min_kib", 1024},
     {nullptr, "test_d2h_delay_us", 0},
 };
 

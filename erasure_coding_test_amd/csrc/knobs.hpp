@@ -35,6 +35,9 @@ enum class Knob : int {
   kPipeD2hWorker,   // ECGPU_PIPE_D2H_WORKER: pipelines issue pageable D2H from a worker thread
   kPacket,          // ECGPU_PACKET: packet kernel, 0 production, 1 8-B lanes, 2 unpipelined 16-B
   kShardSkewKib,    // ECGPU_SHARD_SKEW_KIB: one shard skew for every size (-1 = the measured table)
+  kSplit,           // ECGPU_SPLIT: synchronous host-memory calls cut into byte ranges run concurrently,
+                    // 0 off, -1 one range per visible device, N > 0 N ranges over the devices in turn
+  kSplitMinKib,     // ECGPU_SPLIT_MIN_KIB: smallest range of a split call
   kTestD2hDelayUs,  // tests only, set with ecgpu_set_knob (no environment variable): the D2H
                     // worker sleeps this long before issuing a job (widens a race window)
   kCount

@@ -251,6 +251,46 @@ def dropin_pinned(k=10, m=4, S=4 << 20, reps=10):
             "decode_ms": round(td * 1e3, 3), "decode_ok": bool(torch.equal(bufs[0], saved))}
 
 
+def dropin_split(reps=5, rounds=3):
+    """Synchronous jerasure_matrix_encode on host buffers with the call split
+    into byte ranges run concurrently (ECGPU_SPLIT = 0 / 2 / 4 / 8; on one GPU
+    every range shares its link), pageable and pinned, C3 RS(10,4) 4 MiB and
+    C5 RS(12,4) 16 MiB; interleaved rounds, medians."""
+    from erasure_coding_test_amd import _native as N
+    out = {}
+    for k, m, S in ((10, 4, 4 << 20), (12, 4, 16 << 20)):
+        M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+        for pinned in (False, True):
+            if pinned:
+                data = [torch.randint(0, 256, (S,), dtype=torch.uint8).pin_memory() for _ in range(k)]
+                coding = [torch.zeros(S, dtype=torch.uint8).pin_memory() for _ in range(m)]
+            else:
+                rng = np.random.default_rng(k)
+                data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+                coding = [np.zeros(S, np.uint8) for _ in range(m)]
+            times = {w: [] for w in (0, 2, 4, 8)}
+            ref = None
+            for _ in range(rounds):
+                for ways in times:
+                    N.set_knob("split", ways)
+                    N.set_knob("split_min_kib", 256)
+                    E.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, S)
+                    t0 = time.perf_counter()
+                    for _ in range(reps):
+                        E.jerasure.jerasure_matrix_encode(k, m, 8, M, data, coding, S)
+                    times[ways].append((time.perf_counter() - t0) / reps)
+                    got = [bytes(np.asarray(c)[:4096]) + bytes(np.asarray(c)[-4096:]) for c in coding]
+                    ref = ref or got
+                    assert got == ref, ("split result differs", ways)
+            N.reset_knob("split")
+            N.reset_knob("split_min_kib")
+            key = f"RS({k},{m}) {S >> 20} MiB {'pinned' if pinned else 'pageable'}"
+            out[key] = {f"split{w}_ms": round(sorted(t)[len(t) // 2] * 1e3, 3) for w, t in times.items()}
+            out[key].update({f"split{w}_data_GiBps": round(k * S / sorted(t)[len(t) // 2] / GiB, 2)
+                             for w, t in times.items()})
+    return out
+
+
 def ecx_accum(k=10, m=4, S=4 << 20, stripes=12):
     """ECX incremental accumulation (ecx_datanode_main.cpp:680-735) through
     ParityAccumulator: per stripe, k synchronous adds (one arriving source
@@ -387,6 +427,7 @@ def main():
              "dropin_pageable": dropin_pageable,
              "dropin_pinned": dropin_pinned,
              "dropin_pinned_c2": lambda: dropin_pinned(6, 3, 1 << 20, 50),
+             "dropin_split": dropin_split,
              "ecx_accum": ecx_accum,
              "call_latency": call_latency,
              "device_configs": device_configs}

@@ -175,6 +175,91 @@ __global__ __launch_bounds__(kBlock) void gf_xor_packets16p(PacketArgs a) {
     if (r < a.R) store16t<1>(a.dst[r] + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
 }
 
+// Unit form of the 16-B kernel for the map of every w = 8 Vandermonde
+// bit-matrix encode (jerasure_matrix_to_bitmatrix of reed_sol's matrix,
+// whose row 0 and column 0 are all ones, reed_sol.cpp:324-349): 32 output
+// rows (4 coding devices x 8), sources device-major (j = 8 * device + bit),
+// and the identity blocks of coefficient 1 -- output row b of coding device 0
+// is fed by bit b of every data device, and data device 0's bit b feeds row b
+// of every coding device -- checked exactly on the masks by the host per
+// launch (packets.hip unit_packet_map).  Those terms become plain XORs into a
+// compile-time row: 4 VALU per source row instead of 32 for rows 0..7, and 16
+// instead of 128 for device 0's rows (RS(10,4): 7,328 instead of 10,240 VALU
+// per lane; the 32-row kernel is VALU-bound, profiles/r04_pmc_packets.json).
+// A chunk of four source rows holds bits 0..3 (even chunks) or 4..7 (odd),
+// so the double-buffered loop keeps every bit compile-time.
+// Data device 0's four source rows of bits B0..B0+3: identity blocks, one XOR
+// into row 8g + b of every coding device g.
+template <int B0>
+__device__ __forceinline__ void xor_dev0_4(uint32_t (&acc)[32][4], const u32x4 (&x)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[8 * g + B0 + u][c] ^= x[u][c];
+}
+
+// Any other device's rows of bits B0..B0+3: row b of coding device 0 by XOR,
+// rows 8..31 by their masks.
+template <int B0>
+__device__ __forceinline__ void xor_unit4(uint32_t (&acc)[32][4], const u32x4 (&x)[4], const uint32_t (&m)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[B0 + u][c] ^= x[u][c];
+#pragma unroll
+    for (int r = 8; r < 32; ++r) {
+      const uint32_t sel = uint32_t(int32_t(m[u] << (31 - r)) >> 31);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = __builtin_amdgcn_bitop3_b32(acc[r][c], x[u][c], sel, 0x78);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// WPE: minimum waves per SIMD asked of the register allocator (3: 168 VGPRs
+// with a 12-B spill, as the general kernel's 166; 1: 170 VGPRs, 2 waves).
+template <int RT = 32, int WPE = 3>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_xor_packets16u(PacketArgs a) {
+  static_assert(RT == 32, "the unit form is the 4 x 8-row map of an RS(k, 4) w = 8 encode");
+  const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= a.ncols) return;
+  int64_t sp, col;
+  packet_coords(a, g, &sp, &col);
+  const int64_t soff = sp * a.sstride + col * 16, doff = sp * a.dstride + col * 16;
+  uint32_t acc[32][4];
+#pragma unroll
+  for (int r = 0; r < 32; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+  const int nc = a.nsrc >> 2;  // even: 8 source rows per data device
+  u32x4 xa[4], xb[4];
+  uint32_t ma[4], mb[4];
+  auto load4 = [&](u32x4 (&x)[4], uint32_t (&m)[4], int c) {
+    const int b = (c < nc ? c : nc - 1) * 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      m[u] = kload(a.mask, b + u);
+      x[u] = load16t<1>(kload(a.src, b + u) + soff, 0);
+    }
+  };
+  // chunk 2d holds bits 0..3 of data device d, chunk 2d + 1 bits 4..7;
+  // device 0 first (its rows need no masks), then the double-buffered loop
+  load4(xa, ma, 0);
+  load4(xb, mb, 1);
+  xor_dev0_4<0>(acc, xa);
+  load4(xa, ma, 2);
+  xor_dev0_4<4>(acc, xb);
+  for (int c = 2; c < nc; c += 2) {
+    load4(xb, mb, c + 1);
+    xor_unit4<0>(acc, xa, ma);
+    load4(xa, ma, c + 2);
+    xor_unit4<4>(acc, xb, mb);
+  }
+#pragma unroll
+  for (int r = 0; r < 32; ++r)
+    store16t<1>(kload(a.dst, r) + doff, 0, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+}
+
 // Byte form for packet sizes / bases that are not 8-byte aligned.
 [[maybe_unused]] static __global__ __launch_bounds__(kBlock) void gf_xor_packets_bytes(PacketArgs a) {
   const int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x;

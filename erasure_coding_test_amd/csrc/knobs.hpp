@@ -33,7 +33,8 @@ enum class Knob : int {
   kInline,          // ECGPU_INLINE: one-stripe calls carry pointers and tables in the kernel arguments
   kPipe2d,          // ECGPU_PIPE_2D: evenly spaced host shards cross PCIe as one 2-D copy
   kPipeD2hWorker,   // ECGPU_PIPE_D2H_WORKER: pipelines issue pageable D2H from a worker thread
-  kPacket,          // ECGPU_PACKET: packet kernel, 0 production, 1 8-B lanes, 2 unpipelined 16-B
+  kPacket,          // ECGPU_PACKET: packet kernel, 0 production (unit form where the map allows), 1 8-B
+                    // lanes, 2 unpipelined 16-B, 3 the general pipelined 16-B kernel only
   kShardSkewKib,    // ECGPU_SHARD_SKEW_KIB: one shard skew for every size (-1 = the measured table)
   kSplit,           // ECGPU_SPLIT: synchronous host-memory calls cut into byte ranges run concurrently,
                     // 0 off, -1 one range per visible device, N > 0 N ranges over the devices in turn

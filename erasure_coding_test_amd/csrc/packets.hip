@@ -45,6 +45,21 @@ constexpr int kMaxPacketRow = (1 << 20) - 1;
 
 constexpr int kPacketRows = 32;  // output packet rows per launch (uint32 masks)
 
+// The map of a w = 8 Vandermonde bit-matrix encode, exactly (the unit form
+// gf_xor_packets16u relies on it): 32 output rows, sources device-major in
+// whole devices of 8 bits, bit b of every device feeding output row b (the
+// identity blocks of coding device 0) and device 0's bit b feeding row b of
+// every coding device.
+bool unit_packet_map(const uint32_t* m, int nsrc) {
+  if (nsrc < 8 || nsrc % 8 != 0) return false;
+  for (int j = 0; j < nsrc; ++j) {
+    const uint32_t bit = 1u << (j % 8);
+    if ((m[j] & 0xFFu) != bit) return false;
+    if (j < 8 && m[j] != bit * 0x01010101u) return false;
+  }
+  return true;
+}
+
 // Slot s's packet row r of super-packet sp is ptrs[s] + sp * spstride + r * ps.
 int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride, int64_t ps,
                     const char* call) {
@@ -115,14 +130,29 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
   std::vector<const uint8_t*> sb(static_cast<size_t>(nsrc));
   std::vector<uint8_t*> db(static_cast<size_t>(rows));
   const int64_t temp_stride = (nsp * ps + 255) & ~int64_t(255);
-  for (int j = 0; j < nsrc; ++j) sb[size_t(j)] = base[size_t(pslot(op.srcs[size_t(j)]))] + prow(op.srcs[size_t(j)]) * ps;
+  // sources in (slot, packet row) order -- device-major, bit-minor for a
+  // bit-matrix call, whatever order the tracker met them in -- so the map of
+  // a Vandermonde encode has the layout the unit kernel checks for (the
+  // XOR of the sources does not depend on their order)
+  std::vector<int> sorder(static_cast<size_t>(nsrc));
+  for (int j = 0; j < nsrc; ++j) sorder[size_t(j)] = j;
+  std::stable_sort(sorder.begin(), sorder.end(), [&](int x, int y) {
+    const void* kx = op.srcs[size_t(x)];
+    const void* ky = op.srcs[size_t(y)];
+    return pslot(kx) != pslot(ky) ? pslot(kx) < pslot(ky) : prow(kx) < prow(ky);
+  });
+  for (int j = 0; j < nsrc; ++j) {
+    const void* key = op.srcs[size_t(sorder[size_t(j)])];
+    sb[size_t(j)] = base[size_t(pslot(key))] + prow(key) * ps;
+  }
   for (int r = 0; r < rows; ++r)
     db[size_t(r)] = via_temp ? c->stage + temp_off + size_t(r) * size_t(temp_stride)
                              : base[size_t(pslot(op.dsts[size_t(r)]))] + prow(op.dsts[size_t(r)]) * ps;
   std::vector<uint32_t> masks(size_t(nsrc) * ngroups, 0u);
   for (int r = 0; r < rows; ++r)
     for (int j = 0; j < nsrc; ++j)
-      if (op.coef[size_t(r) * nsrc + j]) masks[size_t(r / kPacketRows) * nsrc + j] |= 1u << (r % kPacketRows);
+      if (op.coef[size_t(r) * nsrc + sorder[size_t(j)]])
+        masks[size_t(r / kPacketRows) * nsrc + j] |= 1u << (r % kPacketRows);
   // one upload of [src bases | dst bases | masks]
   std::vector<uint8_t> host_tab(tab_bytes);
   std::memcpy(host_tab.data(), sb.data(), sizeof(void*) * nsrc);
@@ -138,8 +168,9 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
   bool aligned = ps % 8 == 0 && spstride % 8 == 0 && dstride % 8 == 0;
   for (auto* p : sb) aligned &= (reinterpret_cast<uintptr_t>(p) & 7u) == 0;
   for (auto* p : db) aligned &= (reinterpret_cast<uintptr_t>(p) & 7u) == 0;
-  // 16-B lanes when everything is 16-B aligned; ECGPU_PACKET=1 forces 8-B
-  // lanes, 2 the unpipelined 16-B kernel (A/B, RS(10,4) w = 8 64 MiB
+  // 16-B lanes when everything is 16-B aligned, in the unit form when the map
+  // is a Vandermonde encode's; ECGPU_PACKET=1 forces 8-B lanes, 2 the
+  // unpipelined 16-B kernel, 3 the general pipelined 16-B kernel (A/B, RS(10,4) w = 8 64 MiB
   // bit-matrix encode on MI355X: pipelined 16-B lanes 180.5 us, unpipelined
   // with 8 rows in flight 187, 8-B lanes 190; profiles/r02_packet_ab.txt)
   const int packet_kind = knob(Knob::kPacket);
@@ -165,7 +196,10 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
       continue;
     }
     void* fn = nullptr;
-    if (wide16 && packet_kind == 2)
+    if (wide16 && packet_kind == 0 && R == kPacketRows &&
+        unit_packet_map(masks.data() + size_t(g0) * nsrc, nsrc))
+      fn = reinterpret_cast<void*>(&dev::gf_xor_packets16u<32>);
+    else if (wide16 && packet_kind == 2)
       fn = R <= 8    ? reinterpret_cast<void*>(&dev::gf_xor_packets16<8, 8>)
            : R <= 16 ? reinterpret_cast<void*>(&dev::gf_xor_packets16<16, 8>)
                      : reinterpret_cast<void*>(&dev::gf_xor_packets16<32, 8>);

@@ -1144,7 +1144,31 @@ def test_bitmatrix_coding_device(ec, gpu, k, m, w, ps):
         assert np.array_equal(dc[i].cpu().numpy(), want[i]), i
 
 
-@pytest.mark.parametrize("kind", ["0", "1", "2"])  # ECGPU_PACKET: pipelined 16-B, 8-B lanes, unpipelined 16-B
+@pytest.mark.parametrize("kind", ["0", "3"])  # ECGPU_PACKET: unit form where the map allows, general 16-B kernel
+@pytest.mark.parametrize("k", [1, 2, 6, 10, 12])
+def test_vandermonde_bitmatrix_unit_form(ec, gpu, knobs, kind, k):
+    """The w = 8 Vandermonde bit-matrix encode of RS(k,4): the unit-structure
+    packet kernel (identity blocks of coding device 0 and data device 0 as
+    plain XORs) and the general kernel, against the numpy restatement."""
+    import torch
+    knobs.set("ECGPU_PACKET", kind)
+    m, w, ps = 4, 8, 1024
+    J = ec.jerasure
+    bm = J.jerasure_matrix_to_bitmatrix(k, m, w, ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, w))
+    size = w * ps * 5
+    rng = np.random.default_rng(700 + k)
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)]
+    want = _np_bitmatrix_encode(k, m, w, bm, data, size, ps)
+    dd = [torch.from_numpy(a).to(gpu) for a in data]
+    dc = [torch.full((size,), 0x5A, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    J.jerasure_bitmatrix_encode(k, m, w, bm, dd, dc, size, ps)
+    torch.cuda.synchronize()
+    for i in range(m):
+        assert np.array_equal(dc[i].cpu().numpy(), want[i]), i
+
+
+@pytest.mark.parametrize("kind", ["0", "1", "2", "3"])  # ECGPU_PACKET: production, 8-B lanes, unpipelined 16-B,
+#                                                         general pipelined 16-B
 @pytest.mark.parametrize("k,m,w,ps", [(1, 1, 3, 64), (5, 2, 3, 128), (3, 2, 5, 16), (10, 4, 8, 2048),
                                       (7, 5, 2, 48), (4, 3, 3, 8), (3, 3, 3, 5)])
 def test_random_bitmatrix_packet_kernels(ec, gpu, knobs, kind, k, m, w, ps):

@@ -428,6 +428,8 @@ def main():
              "dropin_pinned": dropin_pinned,
              "dropin_pinned_c2": lambda: dropin_pinned(6, 3, 1 << 20, 50),
              "dropin_split": dropin_split,
+             "pipeline_depth": lambda: {f"depth{d}_round{r}": e2e_pipeline(a.stripes, depth=d)["data_GiBps"]
+                                        for r in range(2) for d in (2, 3, 4, 6)},
              "ecx_accum": ecx_accum,
              "call_latency": call_latency,
              "device_configs": device_configs}

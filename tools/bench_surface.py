@@ -74,6 +74,10 @@ def main():
     for ps in (1024, 4096, 65536):
         rec(f"jerasure_bitmatrix_encode w=8 packetsize={ps}",
             lambda ps=ps: J.jerasure_bitmatrix_encode(k, m, 8, bm, data, coding, S, ps))
+    N.set_knob("ECGPU_PACKET", 3)  # the general pipelined 16-B kernel (no unit form)
+    rec("jerasure_bitmatrix_encode w=8 packetsize=4096 (general kernel, ECGPU_PACKET=3)",
+        lambda: J.jerasure_bitmatrix_encode(k, m, 8, bm, data, coding, S, 4096))
+    N.reset_knob("ECGPU_PACKET")
     sched = J.jerasure_dumb_bitmatrix_to_schedule(k, m, 8, bm)
     rec("jerasure_schedule_encode (dumb) w=8 packetsize=4096",
         lambda: J.jerasure_schedule_encode(k, m, 8, sched, data, coding, S, 4096))

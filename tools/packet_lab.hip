@@ -9,7 +9,7 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I erasure_coding_test_amd/csrc \
 //     tools/packet_lab.hip erasure_coding_test_amd/csrc/gf_host.cpp erasure_coding_test_amd/csrc/matrix_host.cpp \
 //     -o tools/packet_lab.bin
-//   tools/packet_lab.bin [--mib 64] [--ps 4096] [--rounds 9] [--reps 10] [--skew-kib N]
+//   tools/packet_lab.bin [--mib 64] [--ps 4096] [--rounds 9] [--reps 10] [--skew-kib N] [--only name,name]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -253,8 +253,10 @@ struct Variant {
 
 int main(int argc, char** argv) {
   int mib = 64, ps = 4096, rounds = 9, reps = 10, skew_kib = -1;
+  std::string only;  // --only a,b: time only the variants whose names contain one of these (the first always runs)
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string f = argv[i];
+    if (f == "--only") only = argv[i + 1];
     if (f == "--mib") mib = std::atoi(argv[i + 1]);
     else if (f == "--ps") ps = std::atoi(argv[i + 1]);
     else if (f == "--rounds") rounds = std::atoi(argv[i + 1]);
@@ -322,6 +324,22 @@ int main(int argc, char** argv) {
   vs.push_back({"ring_c8x2", reinterpret_cast<const void*>(&lab::packets16_ring<32, 8, 2>)});
   vs.push_back({"ring_c8x3", reinterpret_cast<const void*>(&lab::packets16_ring<32, 8, 3>)});
   vs.push_back({"ring_c6x3", reinterpret_cast<const void*>(&lab::packets16_ring<32, 6, 3>)});
+  vs.push_back({"prod_unit16u", reinterpret_cast<const void*>(&gf_xor_packets16u<32, 3>)});
+  vs.push_back({"unit16u_wpe1", reinterpret_cast<const void*>(&gf_xor_packets16u<32, 1>)});
+  vs.push_back({"probe_halfvalu", reinterpret_cast<const void*>(&lab::packets16p_halfvalu<32>), 0, 1, false});
+  if (!only.empty()) {  // keep variant 0 (the reference) and the named ones
+    std::vector<Variant> keep{vs[0]};
+    for (size_t v = 1; v < vs.size(); ++v)
+      for (size_t p0 = 0; p0 <= only.size();) {
+        const size_t p1 = std::min(only.find(',', p0), only.size());
+        if (vs[v].name.find(only.substr(p0, p1 - p0)) != std::string::npos) {
+          keep.push_back(vs[v]);
+          break;
+        }
+        p0 = p1 + 1;
+      }
+    vs = keep;
+  }
   (void)lds_cu;
   auto launch = [&](const Variant& v) {
     PacketArgs args = a;

@@ -58,6 +58,8 @@ def test_fuzz_sync_calls_vs_reference(ec, gpu, reference):
     rng = np.random.default_rng(20261016)
     kinds = {"encode": 0, "decode": 0, "region": 0, "dotprod": 0}
     for case in range(cases):
+        if case and case % 2000 == 0:  # progress for long runs under `pytest -s` (a silent run looks hung)
+            print(f"fuzz: {case}/{cases} cases", flush=True)
         kind = ("encode", "decode", "region", "dotprod")[int(rng.integers(0, 4))]
         where = ("device", "pageable", "pinned")[int(rng.integers(0, 3))]
         size = int(rng.choice(SIZES))
@@ -162,6 +164,8 @@ def test_fuzz_aliased_calls_vs_reference(ec, gpu, reference):
     rng = np.random.default_rng(4242)
     done = {"encode": 0, "dotprod": 0, "decode": 0, "region": 0, "rejected": 0}
     for case in range(cases):
+        if case and case % 500 == 0:
+            print(f"alias fuzz: {case}/{cases} cases", flush=True)
         kind = ("encode", "dotprod", "decode", "region")[int(rng.integers(0, 4))]
         where = ("device", "pageable")[int(rng.integers(0, 2))]
         size = int(rng.choice([8, 4096, 65536 + 8, 262144, (1 << 20) + 8]))

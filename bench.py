@@ -548,17 +548,19 @@ def with_mix(entry, mix):
     return entry
 
 
-def e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes: int = 24, depth: int = 3):
+def e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes: int = 24, depth: int = 3, sync=None):
     """The north star's PCIe-inclusive rate (never `value`): `stripes` stripes
     of pinned host shards through the host pipelines, i.e. H2D, code and D2H
     of consecutive stripes overlapped on three HIP streams (client write path
     client_main.cpp:1714-1815: data in, parity out; read path :2055-2182:
-    survivors in, the erased shards out).  Rank 0 only, after every rank's
-    timed work: the link and the host memory are not shared with the timed
-    region.  Data GiB/s = k * S per stripe over the wall time of one pass
-    (the first pass warms the pipelines); the last stripe's parity is checked
-    against a device-resident encode of the same data, the decode against the
-    shards it rebuilt."""
+    survivors in, the erased shards out).  After every rank's timed work: the
+    link and the host memory are not shared with the timed region.  At N = 1
+    rank 0 runs it after the CPU baselines; at N > 1 every rank runs it on its
+    own GPU at once (e2e_all_ranks), `sync` -- a barrier -- starting each
+    timed pass together.  Data GiB/s = k * S per stripe over the wall time of
+    one pass (the first pass warms the pipelines); the last stripe's parity is
+    checked against a device-resident encode of the same data, the decode
+    against the shards it rebuilt."""
     import torch
     host = torch.empty((stripes, k + m, S), dtype=torch.uint8).pin_memory()
     g = torch.Generator(device=dev).manual_seed(0xE2E)
@@ -574,13 +576,16 @@ def e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes: int = 24, depth: i
                 p.submit([host[s, j] for j in range(k)], [host[s, k + i] for i in range(m)])
             p.drain()
         run()
+        if sync is not None:
+            sync()
         t0 = time.perf_counter()
         run()
         return time.perf_counter() - t0
 
     out = {"workload": f"RS({k},{m}) {S >> 20} MiB shards, {stripes} stripes of pinned host memory, "
                        f"pipeline depth {depth}, one GPU's PCIe link",
-           "unit": "GiB/s of data shards", "note": "PCIe-inclusive; not the bench value (inputs resident in HBM)"}
+           "unit": "GiB/s of data shards", "note": "PCIe-inclusive; not the bench value (inputs resident in HBM)",
+           "stripes": stripes, "data_bytes_per_pass": stripes * k * S, "host_numa_node": page_numa_node(host.data_ptr())}
     enc = E.HostPipeline(k, m, M, S, depth=depth, device=dev.index)
     t = timed_pass(enc)
     enc.close()
@@ -601,6 +606,92 @@ def e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes: int = 24, depth: i
                          "pass_ms": round(t * 1e3, 2), "rebuilt_ok": bool(torch.equal(host[stripes - 1], want))}
     del host
     return out
+
+
+# ------------------------------------------------------- NUMA placement ----
+def pci_numa_node(bus_id, sysfs="/sys/bus/pci/devices"):
+    """The NUMA node a PCI device (a GPU, by its bus id) hangs off, or None."""
+    if not bus_id:
+        return None
+    try:
+        with open(os.path.join(sysfs, bus_id.lower(), "numa_node")) as f:
+            n = int(f.read().strip())
+        return n if n >= 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def parse_cpulist(text: str) -> set:
+    """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11}"""
+    out = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def node_cpus(node, sysfs="/sys/devices/system/node"):
+    try:
+        with open(os.path.join(sysfs, f"node{node}", "cpulist")) as f:
+            return parse_cpulist(f.read())
+    except (OSError, ValueError):
+        return set()
+
+
+def page_numa_node(addr: int):
+    """The NUMA node holding the page at `addr` (move_pages(2) query), or None."""
+    import ctypes
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        page = ctypes.c_void_p(addr & ~(os.sysconf("SC_PAGE_SIZE") - 1))
+        status = ctypes.c_int(-1)
+        sys_move_pages = 279  # x86-64
+        rc = libc.syscall(ctypes.c_long(sys_move_pages), 0, ctypes.c_ulong(1), ctypes.byref(page), None,
+                          ctypes.byref(status), 0)
+        return int(status.value) if rc == 0 and status.value >= 0 else None
+    except (OSError, AttributeError, ValueError):
+        return None
+
+
+def e2e_aggregate(per_rank: list) -> dict:
+    """Whole-job PCIe-inclusive rate at N > 1: every rank's pass bytes over the
+    slowest rank's pass time (the ranks start each pass together)."""
+    out = {"unit": "GiB/s of data shards, all ranks", "ranks": len(per_rank),
+           "note": "sum of the ranks' data bytes / the slowest rank's pass time; each timed pass starts on a barrier"}
+    for leg in ("encode", "decode"):
+        legs = [r.get(leg) for r in per_rank]
+        if not legs or any(x is None for x in legs):
+            continue
+        total = sum(r["data_bytes_per_pass"] for r in per_rank)
+        slowest = max(x["pass_ms"] for x in legs) / 1e3
+        ok = all(x.get("parity_ok", x.get("rebuilt_ok", True)) for x in legs)
+        out[leg] = {"data_GiBps": round(total / slowest / 2**30, 2), "slowest_pass_ms": round(slowest * 1e3, 2),
+                    "per_rank_GiBps": [x["data_GiBps"] for x in legs], "ok": bool(ok)}
+    return out
+
+
+def e2e_all_ranks(E, M, k, m, S, erasures, dev, local, world, stripes):
+    """N > 1: every rank's e2e pass on its own GPU and PCIe link at once, with
+    the rank's threads (and so the first touch of its pinned buffers) on the
+    NUMA node its GPU hangs off, when the host tells which that is."""
+    import ctypes
+    from erasure_coding_test_amd import _native as N
+    buf = ctypes.create_string_buffer(64)
+    bus = buf.value.decode() if N.lib.ecgpu_device_pci_bus_id(local, buf, len(buf)) == 0 else None
+    gpu_node = pci_numa_node(bus)
+    before = os.sched_getaffinity(0)
+    near = (node_cpus(gpu_node) & before) if gpu_node is not None else set()
+    if near:
+        os.sched_setaffinity(0, near)
+    try:
+        r = e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes=stripes, sync=lambda: barrier(world))
+    finally:
+        os.sched_setaffinity(0, before)
+    r["gpu_numa_node"] = gpu_node
+    r["threads_on_gpu_node"] = bool(near)
+    return r
 
 
 def load_traffic(name: str, workload_key: str, kernel_id: str, profiles_dir: str = ""):
@@ -624,7 +715,14 @@ def load_traffic(name: str, workload_key: str, kernel_id: str, profiles_dir: str
     return d.get("hbm_bytes_per_launch"), f"{d.get('from')} (kernel build {kernel_id})"
 
 
-CFG_WARMUP, CFG_REPS = 5, 20  # per configs-block entry (profiles/summarize.py relies on these counts)
+# Per configs-block entry (profiles/summarize.py relies on these counts).  The
+# warm-up covers the DVFS transient a new back-to-back load starts with: the
+# first 3-4 launches run at boost clock, the chip then drops its clock (1.5 GHz
+# effective at launches 3-8) and recovers over ~20 launches; the multiply-dense
+# C4 decode turns issue-bound in the dip (profiles/r05_c4_spread.json), so 5
+# warm-ups left it timed inside the recovery.  25 puts every config at its
+# settled clock, like the probes that time them in-process.
+CFG_WARMUP, CFG_REPS = 25, 20
 C3_RANDOM_DATA_ERASURE_SEED = 0xC3
 
 
@@ -835,7 +933,10 @@ def main(argv=None):
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
 
     # B stripes x (k+m) shards in one HBM slab at the library's recommended
-    # shard stride (S + 10 KiB skew); global stripe ids round-robin over ranks
+    # shard stride, ecgpu_recommended_shard_stride(S) = round_up(S, 256) + the
+    # skew csrc/shard_stride.hpp measured for S (6 KiB at 4 MiB, 8 KiB at 16 MiB;
+    # the line records it as config.shard_stride_bytes); global stripe ids
+    # round-robin over ranks
     ids = global_stripe_ids(B, rank, world)
     slab, shards = E.alloc_stripes(B, k, m, S, dev)
     shard_stride = int(slab.stride(1))
@@ -933,6 +1034,13 @@ def main(argv=None):
     c5 = None
     if not args.no_configs and args.config == "C3":
         c5 = sharded_c5(E, N, dev, stream, kind, bool(args.nt), rank, world)
+    # about 1.5 GiB of pinned host memory per rank at most (C3: 24 stripes, C5: 6)
+    e2e_n = min(args.e2e_stripes, max(2, (3 << 29) // ((k + m) * S)))
+    e2e_mine = None
+    if world > 1 and args.e2e_stripes > 0:
+        barrier(world)
+        e2e_mine = e2e_all_ranks(E, M, k, m, S, erasures, dev, local, world, e2e_n)
+        barrier(world)
 
     enc_frac = enc_bytes / (enc_ms / 1e3) / 1e9 / HBM_PEAK_GBS
     mine = {"rank": rank, "device": local, **device_identity(N, local), "elapsed_s": round(elapsed, 6),
@@ -946,8 +1054,14 @@ def main(argv=None):
     if configs:
         mine["configs"] = {name: {"median_launch_ms": e["median_launch_ms"], "frac": e["frac"]}
                            for name, e in configs.items()}
+    if e2e_mine is not None:
+        mine["e2e"] = e2e_mine
+    # no GPU result may come from the drop-in's CPU fallback; the
+    # package keeps it off, and a nonzero count fails the run
+    mine["cpu_fallbacks"] = N.fallback_count()
     per_rank = gather(mine, world)
-    ok = all(p["parity_ok"] for p in per_rank) and (c5 is None or c5["parity_ok"])
+    ok = (all(p["parity_ok"] for p in per_rank) and (c5 is None or c5["parity_ok"]) and
+          all(p["cpu_fallbacks"] == 0 for p in per_rank))
     devices_ok, devices_note = distinct_devices(per_rank, rehearsal)
     barrier(world)  # every rank's GPU work is done: the CPU baseline below runs alone
 
@@ -972,11 +1086,16 @@ def main(argv=None):
             if host_has_avx2() and os.path.exists(REFERENCE_O3_SO):
                 cpu_o3, ok_o3 = cpu_baseline(max(2.0, args.cpu_seconds / 2), host_stripe, k, m, erasures, o3=True)
                 cpu_ok = cpu_ok and ok_o3
-        # about 1.5 GiB of pinned host memory at most (C3: 24 stripes, C5: 6)
-        e2e_n = min(args.e2e_stripes, max(2, (3 << 29) // ((k + m) * S)))
-        e2e = e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes=e2e_n) if args.e2e_stripes > 0 else None
+        e2e_per_rank = e2e_agg = None
+        if world > 1:
+            e2e_per_rank = [p.pop("e2e", None) for p in per_rank]
+            e2e = e2e_per_rank[0]
+            e2e_agg = e2e_aggregate(e2e_per_rank) if all(e2e_per_rank) else None
+        else:
+            e2e = e2e_host_pipelines(E, M, k, m, S, erasures, dev, stripes=e2e_n) if args.e2e_stripes > 0 else None
         e2e_ok = (None if not e2e else
-                  bool(e2e["encode"]["parity_ok"] and e2e.get("decode", {}).get("rebuilt_ok", True)))
+                  all(bool(r["encode"]["parity_ok"] and r.get("decode", {}).get("rebuilt_ok", True))
+                      for r in (e2e_per_rank or [e2e])))
         achieved = enc_bytes / (enc_ms / 1e3) / 1e9
         wkey = f"{args.config}:{B}"
         kernel_id = N.lib.ecgpu_build_id(1).decode()
@@ -1028,6 +1147,8 @@ def main(argv=None):
             "cpu_baseline_all_cores": cpu_all,
             "cpu_baseline_o3": cpu_o3,
             "e2e": e2e,
+            **({"e2e_per_rank": e2e_per_rank, "e2e_aggregate": e2e_agg} if world > 1 else {}),
+            "cpu_fallbacks": sum(p["cpu_fallbacks"] for p in per_rank),
             "selfcheck_parity_ok": ok,
             "selfcheck_vs_reference_cpu": cpu_ok,
             "e2e_ok": e2e_ok,

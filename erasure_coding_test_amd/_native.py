@@ -44,6 +44,12 @@ SIGNATURES = {
     "ecgpu_reset_knob": (c_int, [c_char_p]),
     "ecgpu_get_knob": (c_int, [c_char_p, c_int_p]),
     "ecgpu_free": (None, [c_void_p]),
+    "ecgpu_fallback_count": (c_int64, []),
+    "ecgpu_device_lost": (c_int, [c_int]),
+    "ecgpu_set_devices": (c_int, [c_int, c_int_p]),
+    "ecgpu_get_devices": (c_int, [c_int_p, c_int]),
+    "ecgpu_call_device": (c_int, []),
+    "ecgpu_engine_launches": (c_int64, [c_int]),
     "ecgpu_galois_single_multiply": (c_int, [c_int, c_int, c_int]),
     "ecgpu_galois_single_divide": (c_int, [c_int, c_int, c_int]),
     "ecgpu_galois_inverse": (c_int, [c_int, c_int]),
@@ -145,14 +151,55 @@ class EcgpuError(RuntimeError):
     pass
 
 
+# The package's own knob defaults, where they differ from the C library's.
+# ECGPU_CPU_FALLBACK: libjerasure_amd.so completes a host-memory call on the
+# CPU after a HIP error (cpu_fallback.hpp) so a deployed datanode
+# keeps running; this package -- what the tests, smoke() and bench.py drive --
+# fails loudly instead (EcgpuError), so no checked or measured result can come
+# from the CPU.  An ECGPU_CPU_FALLBACK set in the environment wins.
+PACKAGE_KNOB_DEFAULTS = {"ECGPU_CPU_FALLBACK": 0}
+
+
+def _apply_package_defaults(names=None) -> None:
+    for env, value in PACKAGE_KNOB_DEFAULTS.items():
+        if (names is None or env in names) and not os.environ.get(env):
+            lib.ecgpu_set_knob(env.encode(), value)
+
+
+_apply_package_defaults()
+
+
 def set_knob(name: str, value: int) -> None:
     """Override a tuning knob for this process (ecgpu_set_knob; knobs.hpp)."""
     check(lib.ecgpu_set_knob(name.encode(), int(value)), "ecgpu_set_knob")
 
 
 def reset_knob(name=None) -> None:
-    """Back to the environment's value (None: every knob)."""
+    """Back to the environment's value (None: every knob), or the package's
+    default for knobs it sets (PACKAGE_KNOB_DEFAULTS)."""
     check(lib.ecgpu_reset_knob(None if name is None else name.encode()), "ecgpu_reset_knob")
+    if name is None:
+        _apply_package_defaults()
+    else:
+        _apply_package_defaults({n for n in PACKAGE_KNOB_DEFAULTS if name in (n, n[len("ECGPU_"):].lower())})
+
+
+def set_devices(devices) -> None:
+    """ECGPU_DEVICES for this process (ecgpu_set_devices); None or [] unsets."""
+    devices = list(devices or [])
+    check(lib.ecgpu_set_devices(len(devices), (c_int * max(1, len(devices)))(*devices)), "ecgpu_set_devices")
+
+
+def get_devices() -> list:
+    n = lib.ecgpu_get_devices(None, 0)
+    buf = (c_int * max(1, n))()
+    lib.ecgpu_get_devices(buf, n)
+    return list(buf[:n])
+
+
+def fallback_count() -> int:
+    """Synchronous calls completed on the CPU after a HIP error (ecgpu_fallback_count)."""
+    return int(lib.ecgpu_fallback_count())
 
 
 def get_knob(name: str) -> int:

@@ -13,14 +13,14 @@ and the test-only checker under oracle/ (make -C oracle).
 An object is rebuilt when its key changes: a SHA-256 of its compiler command
 line and the bytes of its source and every header (stored beside it as
 <object>.key), so neither a touched-but-unchanged file nor a stale object with
-a newer mtime decides.  The library carries two IDs (ecgpu_build_id):
+a newer mtime decides.  The library carries content IDs (ecgpu_build_id):
   0  the whole library: every source and header under csrc/ + ecgpu.h + flags
      + both compilers' --version
-  1  the coding kernels and their dispatch (gf_kernels / gf_spec / the runtime
-     and planner that pick grids, engines and cache policies) + HIP flags +
-     hipcc --version --
-     the identity a rocprofv3 PMC record of a launch is valid for
-     (profiles/summarize.py writes it, bench.py checks it).
+  1  the w = 8 kernels and their dispatch (gf_kernels_w8.hpp, gf_spec.*,
+     dispatch_w8.hip and the defaults of the knobs it reads) + HIP flags +
+     hipcc --version -- the identity a rocprofv3 PMC record of the bench's
+     launches is valid for (profiles/summarize.py writes it, bench.py checks it)
+  2  the same for the w = 16 / 32 kernels, 3 for the GF(2) packet kernels.
 """
 from __future__ import annotations
 
@@ -41,13 +41,15 @@ ARCH = os.environ.get("ECGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 
-HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp", "contract_host.cpp", "knobs.cpp"]
+HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp", "contract_host.cpp", "knobs.cpp",
+             "cpu_fallback.cpp"]
 # (source, object, extra flags): the specialised kernel table is split into
 # one translation unit per output-row count so the four compile in parallel
-HIP_UNITS = [(f, f + ".o", []) for f in ("ecgpu_runtime.hip", "accum.hip", "pipeline.hip", "packets.hip")] + [
-    ("gf_spec.hip", f"gf_spec_r{r}.hip.o", [f"-DECGPU_SPEC_R={r}"]) for r in (1, 2, 3, 4)]
-HDRS = ["buffer_contract.hpp", "gf_host.hpp", "knobs.hpp", "shard_stride.hpp", "host_sync.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp", "gf_kernels_w8.hpp", "gf_kernels_wide.hpp",
-        "gf_kernels_packets.hpp", "gf_spec.hpp",
+HIP_UNITS = [(f, f + ".o", []) for f in ("ecgpu_runtime.hip", "dispatch_w8.hip", "dispatch_wide.hip", "accum.hip",
+                                           "pipeline.hip", "packets.hip")] + [
+    (f"{t}.hip", f"{t}_r{r}.hip.o", [f"-DECGPU_SPEC_R={r}"]) for t in ("gf_spec", "wide_spec") for r in (1, 2, 3, 4)]
+HDRS = ["buffer_contract.hpp", "cpu_fallback.hpp", "gf_host.hpp", "knobs.hpp", "shard_stride.hpp", "host_sync.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp", "gf_kernels_w8.hpp", "gf_kernels_wide.hpp",
+        "gf_kernels_packets.hpp", "gf_spec.hpp", "wide_spec.hpp", "diag_kernels_w8.hpp",
         "runtime.hpp"]
 DROPIN_SRCS = ["jerasure_dropin.cpp", "jerasure_surface.cpp"]
 
@@ -72,8 +74,28 @@ def _run_parallel(cmds):
             f.result()
 
 
-KERNEL_ID_SRCS = ["gf_kernels.hpp", "gf_kernels_w8.hpp", "gf_kernels_wide.hpp", "gf_kernels_packets.hpp", "gf_spec.hip", "gf_spec.hpp", "ecgpu_runtime.hip", "runtime.hpp", "planner.cpp",
-                  "planner.hpp", "knobs.cpp", "knobs.hpp"]
+# One build ID per kernel family: the kernel code, its
+# instantiation table and its dispatch (grid, residency, engine and cache
+# policy), plus the default values of the knobs that dispatch reads -- so a
+# w = 32 or packet edit leaves the w = 8 ID, which the bench's PMC traffic
+# records are keyed to, unchanged.  The synchronous calls' staging
+# (ecgpu_runtime.hip) and the measurement-only kernels (diag_kernels*) are in
+# no family.
+KERNEL_FAMILIES = {
+    "kernels": (["gf_kernels_w8.hpp", "gf_spec.hip", "gf_spec.hpp", "dispatch_w8.hip"],
+                ["ECGPU_CAP", "ECGPU_BLOCKS_PER_CU", "ECGPU_KERNEL", "ECGPU_NT"]),
+    "wide": (["gf_kernels_w8.hpp", "gf_kernels_wide.hpp", "wide_spec.hip", "wide_spec.hpp", "dispatch_wide.hip"],
+             ["ECGPU_WIDE", "ECGPU_NIB16", "ECGPU_WIDE_UNITS", "ECGPU_WIDE_PIPE", "ECGPU_WIDE16_BPCU",
+              "ECGPU_WIDE16_UNITS"]),
+    "packets": (["gf_kernels_w8.hpp", "gf_kernels_packets.hpp", "packets.hip"], ["ECGPU_PACKET"]),
+}
+
+
+def knob_rows(names) -> list:
+    """The knobs.cpp table rows of these knobs (their defaults), in order."""
+    with open(os.path.join(CSRC, "knobs.cpp")) as f:
+        lines = f.read().splitlines()
+    return [ln.strip() for n in names for ln in lines if ln.strip().startswith('{"%s",' % n)]
 
 
 def _digest(parts, files) -> str:
@@ -106,13 +128,16 @@ def toolchain(compiler: str) -> str:
 
 
 def build_ids() -> dict:
-    """{'build': ..., 'kernels': ...}: 16-hex content IDs (see module doc)."""
+    """{'build', 'kernels' (w = 8), 'wide', 'packets'}: 16-hex content IDs (see
+    the module doc and KERNEL_FAMILIES)."""
     all_srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
-                      if f.endswith((".hip", ".cpp", ".hpp")) and f != "diag_kernels.hip")
+                      if f.endswith((".hip", ".cpp", ".hpp")) and not f.startswith("diag_kernels"))
     hip, cxx = toolchain(HIPCC), toolchain(CXX)
-    return {"build": _digest([ARCH, hip, cxx] + CXXFLAGS + HIPFLAGS,
-                             all_srcs + [os.path.join(INCLUDE, "ecgpu.h")])[:16],
-            "kernels": _digest([ARCH, hip] + HIPFLAGS, [os.path.join(CSRC, f) for f in KERNEL_ID_SRCS])[:16]}
+    ids = {"build": _digest([ARCH, hip, cxx] + CXXFLAGS + HIPFLAGS,
+                            all_srcs + [os.path.join(INCLUDE, "ecgpu.h")])[:16]}
+    for name, (files, knobs) in KERNEL_FAMILIES.items():
+        ids[name] = _digest([ARCH, hip] + HIPFLAGS + knob_rows(knobs), [os.path.join(CSRC, f) for f in files])[:16]
+    return ids
 
 
 def _stale(target, deps, cmd=()):
@@ -152,7 +177,8 @@ def build_native(verbose: bool = True) -> dict:
     objs = []
     for src in HOST_SRCS:
         s, o = os.path.join(CSRC, src), os.path.join(OBJ, src + ".o")
-        extra = ([f'-DECGPU_BUILD_ID="{ids["build"]}"', f'-DECGPU_KERNEL_ID="{ids["kernels"]}"']
+        extra = ([f'-DECGPU_BUILD_ID="{ids["build"]}"', f'-DECGPU_KERNEL_ID="{ids["kernels"]}"',
+                  f'-DECGPU_WIDE_ID="{ids["wide"]}"', f'-DECGPU_PACKETS_ID="{ids["packets"]}"']
                  if src == "capi_host.cpp" else [])
         cmd = [CXX] + CXXFLAGS + extra + ["-fvisibility=hidden", "-c", s, "-o", o]
         if _stale(o, [s] + hdrs, cmd):

@@ -33,14 +33,28 @@ ECGPU_API const char* ecgpu_version(void) { return "ecgpu 0.1 (gfx950)"; }
 ECGPU_API const char* ecgpu_last_error(void) { return rt::t_err.c_str(); }
 
 // Content IDs of this build (erasure_coding_test_amd/build.py): 0 the whole
-// library, 1 the coding kernels and their dispatch.
+// library, 1 the w = 8 kernels and their dispatch, 2 the w = 16 / 32 ones,
+// 3 the GF(2) packet ones.
 #ifndef ECGPU_BUILD_ID
 #define ECGPU_BUILD_ID "unknown"
 #endif
 #ifndef ECGPU_KERNEL_ID
 #define ECGPU_KERNEL_ID "unknown"
 #endif
-ECGPU_API const char* ecgpu_build_id(int what) { return what == 1 ? ECGPU_KERNEL_ID : ECGPU_BUILD_ID; }
+#ifndef ECGPU_WIDE_ID
+#define ECGPU_WIDE_ID "unknown"
+#endif
+#ifndef ECGPU_PACKETS_ID
+#define ECGPU_PACKETS_ID "unknown"
+#endif
+ECGPU_API const char* ecgpu_build_id(int what) {
+  switch (what) {
+    case 1: return ECGPU_KERNEL_ID;
+    case 2: return ECGPU_WIDE_ID;
+    case 3: return ECGPU_PACKETS_ID;
+    default: return ECGPU_BUILD_ID;
+  }
+}
 ECGPU_API void ecgpu_free(void* p) { std::free(p); }
 
 // The shard stride of shard_stride.hpp (the measured per-size skew table).

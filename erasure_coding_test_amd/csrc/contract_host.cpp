@@ -13,7 +13,7 @@
 namespace ecgpu {
 namespace __attribute__((visibility("hidden"))) rt {
 
-int fail(int code, const std::string& msg);  // ecgpu_runtime.hip
+int fail(int code, const std::string& msg);  // capi_host.cpp
 
 // A synchronous call: the buffers the replayed reference sequence named.
 // Identical pointers are one buffer to the tracker (the planner reproduces
@@ -32,9 +32,15 @@ int check_op_buffers(const char* call, const FusedOp& op, int64_t size) {
 }
 
 // One stripe of a host pipeline: the shards it reads (src_ids) and writes
-// (out_ids), id < k in data_ptrs, else coding_ptrs.  The pipeline copies all
-// sources in before any output comes back, so an output may not share bytes
-// with any other shard of the stripe, identical or not.
+// (out_ids), id < k in data_ptrs, else coding_ptrs.  An output may not share
+// bytes with any other shard of the stripe, identical pointers included: the
+// pipeline's plan is fixed when it is created (the coding matrix, or one
+// decode pattern's fused map) and runs every stripe from the ORIGINAL bytes of
+// its sources, whereas the reference's sequence over an output that is also a
+// source reads the bytes it has just written (jerasure.cpp:285-299: coding[0]
+// overwrites an aliased data shard before coding[1] reads it).  Only the
+// synchronous calls replay that order per call (planner.hpp), so only they
+// accept identical pointers.
 int check_stripe_buffers(const char* call, int k, char** data, char** coding, const std::vector<int>& src_ids,
                          const std::vector<int>& out_ids, int64_t size) {
   if (size <= 0 || out_ids.empty()) return ECGPU_OK;

@@ -22,7 +22,7 @@
 
 #include <cstdlib>
 
-#include "gf_kernels.hpp"
+#include "diag_kernels_w8.hpp"
 
 using ecgpu::dev::ApplyArgs;
 using ecgpu::dev::u32x4;

@@ -1,8 +1,9 @@
-// ecgpu_runtime.hip -- device side of include/ecgpu.h: plans, kernel
-// dispatch, staging of host buffers, and the hot-path C ABI.  The ECX
-// accumulators (accum.hip), host pipelines (pipeline.hip) and GF(2) packet
-// coding (packets.hip) build on the helpers this file exports to them
-// through runtime.hpp.
+// ecgpu_runtime.hip -- device side of include/ecgpu.h: plans, contexts,
+// staging of host buffers, the synchronous calls with their failure contract,
+// and the hot-path C ABI.  How a plan launches is dispatch_w8.hip (w = 8) and
+// dispatch_wide.hip (w = 16 / 32).  The ECX accumulators (accum.hip), host
+// pipelines (pipeline.hip) and GF(2) packet coding (packets.hip) build on the
+// helpers this file exports to them through runtime.hpp.
 //
 // Execution model (MI355X-first, not the reference's byte loops):
 //   * every hot-path call is planned on the host into ONE fused
@@ -35,6 +36,7 @@
 #include <vector>
 
 #include "buffer_contract.hpp"
+#include "cpu_fallback.hpp"
 #include "ecgpu.h"
 #include "gf_host.hpp"
 #include "gf_kernels.hpp"
@@ -55,159 +57,41 @@ ECGPU_RT_BEGIN
 // t_err / fail / ecgpu_last_error live in capi_host.cpp (host code, so the
 // host-only checks -- buffer contract, knobs -- report through them too)
 
-
-// ------------------------------------------------------- kernel tables ----
-using KernelFn = void (*)(ApplyArgs);
-
-// Production kernels: gf_apply<K, R, UNITS> specialised at compile time
-// (gf_spec.hpp, one translation unit per R): one 16-B column per lane,
-// 3-bit-slice v_perm multiply, XOR3 via v_bitop3, unit-coefficient
-// structure fixed per launch, non-temporal loads; store policy per launch.
-// Which compile-time unit structure holds exactly for rows [r0, r0+R).
-int unit_variant(const std::vector<uint32_t>& coef, int K, int r0, int R) {
-  bool all = true, col0 = true, row0 = true;
-  for (int r = 0; r < R; ++r)
-    for (int j = 0; j < K; ++j) {
-      const bool one = coef[size_t(r0 + r) * K + j] == 1;
-      all &= one;
-      if (j == 0) col0 &= one;
-      if (r == 0) row0 &= one;
-    }
-  if (all) return 4;
-  return (col0 ? 1 : 0) | (row0 ? 2 : 0);
-}
-
-KernelFn generic_fn(int R) {
-  switch (R) {
-    case 1: return &dev::gf_apply_perm_generic<1>;
-    case 2: return &dev::gf_apply_perm_generic<2>;
-    case 3: return &dev::gf_apply_perm_generic<3>;
-    default: return &dev::gf_apply_perm_generic<4>;
+// Errors after which the device's context is unusable for the rest of the
+// process (a kernel fault, a lost / missing device or driver): the device is
+// marked lost, and with ECGPU_CPU_FALLBACK later synchronous calls on it go
+// straight to the CPU (cpu_fallback.hpp).
+bool sticky(hipError_t e) {
+  switch (e) {
+    case hipErrorNotInitialized:
+    case hipErrorDeinitialized:
+    case hipErrorInsufficientDriver:
+    case hipErrorNoDevice:
+    case hipErrorInvalidDevice:
+    case hipErrorNoBinaryForGpu:
+    case hipErrorECCNotCorrectable:
+    case hipErrorIllegalAddress:
+    case hipErrorLaunchTimeOut:
+    case hipErrorContextIsDestroyed:
+    case hipErrorAssert:
+    case hipErrorLaunchFailure:
+    case hipErrorUnknown:
+      return true;
+    default:
+      return false;
   }
 }
 
-hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ApplyArgs& a, hipStream_t s, unsigned lds_bytes = 0) {
-  void* args[] = {&a};
-  return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, block, args, lds_bytes, s);
-}
-
-// Residency cap for the streaming kernels.  Fewer resident workgroups per CU
-// means fewer DRAM pages open at once across the chip: with each lane reading
-// K shards and writing R, the uncapped kernel (VGPR-limited to 7 blocks/CU)
-// keeps ~28k distinct 4 KiB shard chunks in flight.  What matters is the
-// number of shard streams per lane, K + R: a sweep over eight encode and
-// decode shapes (K + R = 5..16, 64 KiB..16 MiB shards, 3 interleaved rounds,
-// profiles/r02_residency_sweep.json) has 4 blocks/CU best or within 0.3 % of
-// the best for K + R <= 9 and 3 blocks/CU for K + R >= 10; never capping is
-// the worst or near it everywhere (-1.5 % to -7 %).  A launch dense in GF
-// multiplies (decode{0,1,2,3}: 40 non-unit coefficients over 14 shards)
-// needs the occupancy to hide its VALU work and loses 7 %, so such launches
-// stay uncapped (cap_for).  The cap is an unused dynamic LDS allocation of
-// LDS_per_CU / blocks (rounded down to 512 B).  A kernel with static LDS of
-// its own (the LDS engine's tables) gets that much less and a further 4 KiB
-// margin, rounded down to 4 KiB: RS(10,4) at "3 per CU" with 1,280 B of
-// tables, dynamic 52,736 B (1.8 KiB spare) ran at 2 per CU's speed (989 us),
-// 40,960-49,152 B at 902-905 (tools/encode_lab.hip --lds 2).
-// ECGPU_BLOCKS_PER_CU fixes the block count (0 = never cap).
-unsigned residency_lds_bytes(int device, int streams, unsigned static_bytes = 0) {
-  static std::once_flag once;
-  static int per_cu = 0;
-  std::call_once(once, [&] {
-    if (hipDeviceGetAttribute(&per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess)
-      per_cu = 0;
-  });
-  const int fixed = knob(Knob::kBlocksPerCu);
-  const int blocks = fixed >= 0 ? fixed : (streams <= 9 ? 4 : 3);
-  if (blocks <= 0 || per_cu <= 0) return 0;
-  const unsigned total = unsigned(per_cu / blocks) & ~511u;
-  const unsigned reserve = static_bytes ? static_bytes + 4096u : 0u;
-  if (total <= reserve) return 0;
-  const unsigned b = (total - reserve) & (static_bytes ? ~4095u : ~511u);
-  return b + static_bytes > unsigned(per_cu / (blocks + 1)) ? b : 0u;
-}
-
-// Per-launch policy of the production kernel (A/B on MI355X in the bench's
-// back-to-back context, DESIGN.md §5, profiles/r01_policy_ab.json):
-//   * stores non-temporal (loads always are): bench step +4 %, RS(10,4)
-//     encode 0.947 -> 0.889 ms, dense decode +9 %, RS(12,4) +6 %;
-//   * residency cap unless the launch is dense in GF multiplies (more than
-//     2.5 non-unit coefficients per shard touched): decode{0} +9 %, RS(6,3)
-//     +6 %; the 40-multiply decode{0,1,2,3} needs the occupancy (-7 % capped).
-// The store policy is the plan's `nt` field (0 plain, 1 nt -- the default;
-// ECGPU_NT, ecgpu_plan_set_kernel); the cap knob (ECGPU_CAP: 0 = never,
-// 1 = always) overrides the cap rule.
-bool cap_for(int K, int R, int mul_terms) {
-  const int v = knob(Knob::kCap);
-  return v < 0 ? 2 * mul_terms <= 5 * (K + R) : (v != 0);
-}
-
-// Per-coefficient tables.  PERM: word p holds c*(e << 2p) in byte e.  LDS:
-// 16 low-nibble products then 16 high-nibble products.
-// P3 (production, gf_kernels.hpp mul3): T0[e] = c*e and T1[e] = c*(e << 3)
-// for e < 8 as dword pairs (low dword = entries 0..3), T2[e] = c*(e << 6).
-void build_tables(int c, u32x4* q, uint32_t* p3, uint8_t* nib) {
-  const auto& T = gf8().mul[c & 0xFF];
-  uint32_t w[4];
-  for (int p = 0; p < 4; ++p) {
-    w[p] = 0;
-    for (int e = 0; e < 4; ++e) w[p] |= uint32_t(T[e << (2 * p)]) << (8 * e);
+int fail_hip(hipError_t e, const char* what) {
+  if (sticky(e)) {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) d = 0;
+    mark_device_lost(d);
   }
-  *q = u32x4{w[0], w[1], w[2], w[3]};
-  for (int i = 0; i < dev::kP3Words; ++i) p3[i] = 0;
-  for (int e = 0; e < 8; ++e) {
-    p3[e >> 2] |= uint32_t(T[e]) << (8 * (e & 3));
-    p3[2 + (e >> 2)] |= uint32_t(T[e << 3]) << (8 * (e & 3));
-  }
-  for (int e = 0; e < 4; ++e) p3[4] |= uint32_t(T[e << 6]) << (8 * e);
-  for (int x = 0; x < 16; ++x) {
-    nib[x] = T[x];
-    nib[16 + x] = T[x << 4];
-  }
+  return fail(ECGPU_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Wide-word tables (gf_kernels.hpp, "wide words"): for coefficient c of
-// GF(2^(8W)), the v_perm table pairs of every (rotation d, slice p[, lane
-// pair h]).  lane_table(o, b, p) byte e = byte o of c * ((e << 2p) << 8b).
-void build_wide_tables(uint32_t c, int W, uint32_t* t) {
-  const int w = 8 * W;
-  auto lane_table = [&](int o, int b, int p) {
-    uint32_t v = 0;
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t x = uint32_t(e) << (2 * p) << (8 * b);
-      v |= ((gf_mul_poly(x, c, w) >> (8 * o)) & 0xFFu) << (8 * e);
-    }
-    return v;
-  };
-  if (W == 2) {
-    for (int d = 0; d < 2; ++d)
-      for (int p = 0; p < 4; ++p) {
-        const int i = d * 4 + p;
-        t[2 * i] = lane_table(1, (1 + d) % 2, p);  // odd lanes (selectors 4..7)
-        t[2 * i + 1] = lane_table(0, d % 2, p);    // even lanes (selectors 0..3)
-      }
-  } else {
-    for (int d = 0; d < 4; ++d)
-      for (int p = 0; p < 4; ++p)
-        for (int h = 0; h < 2; ++h) {
-          const int i = (d * 4 + p) * 2 + h, lo = 2 * h, hi = 2 * h + 1;
-          t[2 * i] = lane_table(hi, (hi + d) % 4, p);
-          t[2 * i + 1] = lane_table(lo, (lo + d) % 4, p);
-        }
-  }
-}
 
-// LDS nibble tables of gf_apply_wide_nib: T_t[v] = c*(v << 4t) at w = 32; at
-// w = 16 tables 0..3 serve the low word of a dword and 4..7 the high word
-// (entries shifted into bits 16..31).
-void build_wide_nib_tables(uint32_t c, int w, uint32_t* t) {
-  for (int tt = 0; tt < 8; ++tt)
-    for (uint32_t v = 0; v < 16; ++v)
-      t[tt * 16 + int(v)] = w == 32  ? gf_mul_poly(v << (4 * tt), c, 32)
-                            : tt < 4 ? gf_mul_poly(v << (4 * tt), c, 16)
-                                     : gf_mul_poly(v << (4 * (tt - 4)), c, 16) << 16;
-}
-
-int wide_words_per_coef(int w) { return w == 16 ? 2 * dev::Wide<2>::kPerms : 2 * dev::Wide<4>::kPerms; }
 
 ECGPU_RT_END
 
@@ -269,7 +153,7 @@ int plan_wait_tables(ecgpu_plan* p, hipStream_t stream) {
     std::vector<uint8_t>().swap(p->host_tabs);
     return ECGPU_OK;
   }
-  if (q != hipErrorNotReady) return fail(ECGPU_ERR_HIP, std::string("table upload: ") + hipGetErrorString(q));
+  if (q != hipErrorNotReady) return fail_hip(q, "table upload");
   (void)hipGetLastError();  // not ready is not an error
   ECGPU_HIP(hipStreamWaitEvent(stream, p->uploaded, 0));
   return ECGPU_OK;
@@ -296,48 +180,8 @@ int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, i
   p->nt = std::min(kStorePolicies - 1, std::max(0, knob(Knob::kNt)));
   const size_t n = size_t(rows) * nsrc;
   p->coef.resize(n);
-  if (w != 8) {
-    const uint32_t mask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
-    const int nw = wide_words_per_coef(w);
-    std::vector<uint32_t> t(n * size_t(nw));
-    std::vector<uint8_t> cls(n);
-    std::vector<uint32_t> nib(n * size_t(dev::kNibWords));
-    for (size_t i = 0; i < n; ++i) {
-      p->coef[i] = uint32_t(coefs[i]) & mask;
-      cls[i] = p->coef[i] == 0 ? 2 : p->coef[i] == 1 ? 1 : 0;
-      build_wide_tables(p->coef[i], w / 8, &t[i * size_t(nw)]);
-      build_wide_nib_tables(p->coef[i], w, &nib[i * size_t(dev::kNibWords)]);
-    }
-    // [wide tables | nibble tables | classes] in one allocation, one upload
-    const size_t tb = t.size() * sizeof(uint32_t), nb = nib.size() * sizeof(uint32_t);
-    std::vector<uint8_t> host(tb + nb + n);
-    std::memcpy(host.data(), t.data(), tb);
-    std::memcpy(host.data() + tb, nib.data(), nb);
-    std::memcpy(host.data() + tb + nb, cls.data(), n);
-    if (int rc = plan_upload_tables(p, std::move(host))) return rc;
-    p->d_w = reinterpret_cast<uint32_t*>(p->d_tabs);
-    p->d_wnib = reinterpret_cast<uint32_t*>(p->d_tabs + tb);
-    p->d_wcls = p->d_tabs + tb + nb;
-    return ECGPU_OK;
-  }
-  for (size_t i = 0; i < n; ++i) p->coef[i] = uint32_t(coefs[i]) & 0xFFu;
-  std::vector<u32x4> q(n);
-  std::vector<uint32_t> p3(n * dev::kP3Words);
-  std::vector<uint8_t> nib(n * 32);
-  for (size_t i = 0; i < n; ++i) build_tables(coefs[i], &q[i], &p3[i * dev::kP3Words], &nib[i * 32]);
-  // [2-bit tables | 3-bit tables | nibble tables] in one allocation, ONE
-  // asynchronous upload (plan_upload_tables; three blocking copies cost ~12 us
-  // each, tools/hip_overheads.cpp)
-  const size_t qb = n * sizeof(u32x4), pb = p3.size() * sizeof(uint32_t), nb = n * 32;
-  std::vector<uint8_t> host(qb + pb + nb);
-  std::memcpy(host.data(), q.data(), qb);
-  std::memcpy(host.data() + qb, p3.data(), pb);
-  std::memcpy(host.data() + qb + pb, nib.data(), nb);
-  if (int rc = plan_upload_tables(p, std::move(host))) return rc;
-  p->d_q = reinterpret_cast<u32x4*>(p->d_tabs);
-  p->d_p3 = reinterpret_cast<uint32_t*>(p->d_tabs + qb);
-  p->d_nib = p->d_tabs + qb + pb;
-  return ECGPU_OK;
+  if (w != 8) return plan_init_wide(p, coefs);
+  return plan_init_w8(p, coefs);
 }
 
 // With a stream the pointer tables are uploaded asynchronously on it; unless
@@ -385,240 +229,6 @@ int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* co
   return ECGPU_OK;
 }
 
-// CU count (the launch device; the pool is homogeneous).
-int multiprocessors(int device) {
-  static std::once_flag once;
-  static int n = 0;
-  std::call_once(once, [&] {
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) n = 256;
-  });
-  return n;
-}
-
-// Resident workgroups per CU of a kernel at kBlock threads and `lds` bytes
-// of dynamic LDS (cached; the launch shapes are few).
-int resident_blocks(KernelFn fn, unsigned lds) {
-  static std::mutex mu;
-  static std::vector<std::pair<std::pair<const void*, unsigned>, int>> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  const auto key = std::make_pair(reinterpret_cast<const void*>(fn), lds);
-  for (const auto& e : cache)
-    if (e.first == key) return e.second;
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), dev::kBlock, lds) !=
-          hipSuccess ||
-      n <= 0)
-    n = 4;
-  cache.emplace_back(key, n);
-  return n;
-}
-
-// w = 16 / 32: 16-B column kernel over the aligned part, word kernel for the
-// rest; size must be a whole number of words (checked by the callers).  The
-// column kernel is gf_apply_wide_nib (LDS nibble tables) when a launch's
-// tables fit in kNibMaxLds, else gf_apply_wide (v_perm); ECGPU_WIDE=1 forces
-// v_perm (A/B, tools/bench_surface.py).
-int plan_launch_wide(ecgpu_plan* p, hipStream_t stream) {
-  const int K = p->nsrc, W = p->w / 8, nw = wide_words_per_coef(p->w);
-  const int64_t nvec = p->aligned ? p->size / 16 : 0;
-  const int64_t byte0 = nvec * 16;
-  const dim3 block(dev::kBlock);
-  constexpr int kMaxGridY = 65535;
-  const bool force_perm = knob(Knob::kWidePerm) == 1;
-  for (int r0 = 0; r0 < p->rows; r0 += dev::kMaxRows) {
-    const int R = std::min(dev::kMaxRows, p->rows - r0);
-    // w = 16 packs two rows per LDS dword (gf_apply_wide_nib16, half the LDS bytes)
-    const bool pack16 = W == 2 && knob(Knob::kNib16) != 0;
-    // the unit structure (gf_apply_wide_nib<R, 1>, gf_apply_wide_nib16<R, 1>):
-    // the launch's row 0 and column 0 all ones, as in every Vandermonde encode
-    bool unit_rc = R >= 2 && knob(pack16 ? Knob::kWide16Units : Knob::kWideUnits) != 0;
-    for (int j = 0; j < K && unit_rc; ++j) unit_rc = p->coef[size_t(r0) * K + j] == 1u;
-    for (int r = 0; r < R && unit_rc; ++r) unit_rc = p->coef[size_t(r0 + r) * K] == 1u;
-    const unsigned nib_lds =
-        pack16 ? unsigned(K - (unit_rc ? 1 : 0)) * unsigned(dev::nib16_source_bytes(R - (unit_rc ? 1 : 0)))
-               : unsigned(dev::nib_lds_bytes(K, R, unit_rc ? 1 : 0));
-    const bool nib = !force_perm && nib_lds <= unsigned(dev::kNibMaxLds);
-    KernelFn vec_fn = nullptr, word_fn = W == 2 ? &dev::gf_apply_wide_words<2> : &dev::gf_apply_wide_words<4>;
-    if (nib && pack16 && unit_rc) {
-      switch (R) {
-        case 2: vec_fn = &dev::gf_apply_wide_nib16<2, 1>; break;
-        case 3: vec_fn = &dev::gf_apply_wide_nib16<3, 1>; break;
-        default: vec_fn = &dev::gf_apply_wide_nib16<4, 1>; break;
-      }
-    } else if (nib && pack16) {
-      switch (R) {
-        case 1: vec_fn = &dev::gf_apply_wide_nib16<1>; break;
-        case 2: vec_fn = &dev::gf_apply_wide_nib16<2>; break;
-        case 3: vec_fn = &dev::gf_apply_wide_nib16<3>; break;
-        default: vec_fn = &dev::gf_apply_wide_nib16<4>; break;
-      }
-    } else if (nib && unit_rc) {
-      switch (R) {
-        case 2: vec_fn = &dev::gf_apply_wide_nib<2, 1>; break;
-        case 3: vec_fn = &dev::gf_apply_wide_nib<3, 1>; break;
-        default: vec_fn = &dev::gf_apply_wide_nib<4, 1>; break;
-      }
-    } else if (nib) {
-      switch (R) {
-        case 1: vec_fn = &dev::gf_apply_wide_nib<1>; break;
-        case 2: vec_fn = &dev::gf_apply_wide_nib<2>; break;
-        case 3: vec_fn = &dev::gf_apply_wide_nib<3>; break;
-        default: vec_fn = &dev::gf_apply_wide_nib<4>; break;
-      }
-    } else {
-      switch (R) {
-        case 1: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 1> : &dev::gf_apply_wide<4, 1>; break;
-        case 2: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 2> : &dev::gf_apply_wide<4, 2>; break;
-        case 3: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 3> : &dev::gf_apply_wide<4, 3>; break;
-        default: vec_fn = W == 2 ? &dev::gf_apply_wide<2, 4> : &dev::gf_apply_wide<4, 4>; break;
-      }
-    }
-    // The pipelined form of the same kernels (gf_apply_wide_pipe: compile-time
-    // K, the next chunk's loads in flight during this chunk's lookups) for
-    // launches of whole 256-column blocks, where it measured faster: the
-    // w = 32 unit form with K = 7..10 sources (RS(K,4) 64 MiB, in one process:
-    // K = 7 148 -> 139 us, 8 162 -> 149, 10 197 -> 191; K = 5, 11 equal or
-    // slower, and so were the general w = 32 and the w = 16 forms outside
-    // K = 10 -- profiles/r03_wide_lab.jsonl, "r03 pipe K sweep") and, since
-    // round 4, K = 12 in six chunks (227.6 -> 216.8 us,
-    // profiles/r04_wide_lab_k12.jsonl; K = 11 stays level, 210.9 vs 211.0).
-    // ECGPU_WIDE_PIPE: 1 that rule (default), 0 never, 2 every whole-block
-    // launch of every mode (tests, A/B).
-    const int pipe = knob(Knob::kWidePipe);
-    // (the pipelined w = 16 form has no unit structure: it packs every row)
-    const bool pipe_shape = pipe == 2 || (pipe == 1 && !pack16 && unit_rc && ((K >= 7 && K <= 10) || K == 12));
-    bool piped = false;
-    if (nib && nvec > 0 && nvec % dev::kBlock == 0 && pipe_shape)
-      if (KernelFn f = wide_pipe_kernel(K, R, pack16 ? dev::kPipeW16 : unit_rc ? dev::kPipeW32Unit : dev::kPipeW32)) {
-        vec_fn = f;
-        piped = true;
-      }
-    const unsigned launch_lds =
-        piped && pack16 && unit_rc ? unsigned(K) * unsigned(dev::nib16_source_bytes(R)) : nib_lds;
-    for (int s0 = 0; s0 < p->stripes; s0 += kMaxGridY) {
-      const int ns = std::min(kMaxGridY, p->stripes - s0);
-      ApplyArgs a{};
-      a.wtab = nib ? p->d_wnib + size_t(r0) * K * dev::kNibWords : p->d_w + size_t(r0) * K * nw;
-      a.wcls = p->d_wcls + size_t(r0) * K;
-      a.src = p->d_src + size_t(s0) * K;
-      a.dst = p->d_dst + size_t(s0) * p->rows;
-      a.nvec = nvec;
-      a.size = p->size;
-      a.byte0 = byte0;
-      a.src_stride = K;
-      a.dst_stride = p->rows;
-      a.row0 = r0;
-      a.K = K;
-      a.R = R;
-      a.nt = p->nt;
-      if (nvec > 0) {
-        const int64_t nblk = (nvec + dev::kBlock - 1) / dev::kBlock;
-        if (nib) {
-          // exactly one resident round of workgroups (occupancy x CUs), each
-          // looping over column blocks: a second, partial round would run
-          // on part of the chip
-          // The w = 16 packed kernel (LDS at half the w = 32 cycles, HBM-bound)
-          // runs fewer workgroups per CU than fit, like the w = 8 residency
-          // cap: 3 per CU beat the 6 the occupancy allows for RS(10,4) 64 MiB
-          // (171.5 vs 181.6 us), RS(5,4) 64 MiB (107.3 vs 116.0) and RS(12,4)
-          // 16 MiB (55.1 vs 56.3; tools/wide_lab.hip grid sweep,
-          // profiles/r03_wide_lab.jsonl); the LDS-bound w = 32 kernel wants
-          // every wave it can get (3 per CU: 242 vs 192 us).
-          // ECGPU_WIDE16_BPCU overrides (0: the occupancy).
-          int bpcu = resident_blocks(vec_fn, launch_lds);
-          if (pack16) {
-            const int cap16 = knob(Knob::kWide16Bpcu);
-            if (cap16 > 0) bpcu = std::min(bpcu, cap16);
-          }
-          const int64_t per_stripe = std::max<int64_t>(1, int64_t(multiprocessors(p->device)) * bpcu / ns);
-          const dim3 grid(unsigned(std::min(nblk, per_stripe)), unsigned(ns));
-          ECGPU_HIP(launch(vec_fn, grid, block, a, stream, launch_lds));
-        } else {
-          ECGPU_HIP(launch(vec_fn, dim3(unsigned(nblk), unsigned(ns)), block, a, stream));
-        }
-      }
-      const int64_t words = (p->size - byte0) / W;
-      if (words > 0) {
-        // the word kernel reads the v_perm tables
-        a.wtab = p->d_w + size_t(r0) * K * nw;
-        const dim3 grid(unsigned((words + dev::kBlock - 1) / dev::kBlock), unsigned(ns));
-        ECGPU_HIP(launch(word_fn, grid, block, a, stream));
-      }
-    }
-  }
-  return ECGPU_OK;
-}
-
-int plan_launch(ecgpu_plan* p, hipStream_t stream) {
-  if (p->stripes <= 0 || p->size <= 0 || p->rows <= 0) return ECGPU_OK;
-  DeviceGuard g(p->device);
-  if (int rc = plan_wait_tables(p, stream)) return rc;
-  if (p->w != 8) return plan_launch_wide(p, stream);
-  const int K = p->nsrc;
-  const int64_t nvec = p->aligned ? p->size / 16 : 0;
-  const int64_t byte0 = nvec * 16;
-  const dim3 block(dev::kBlock);
-  constexpr int kMaxGridY = 65535;
-  for (int r0 = 0; r0 < p->rows; r0 += dev::kMaxRows) {
-    const int R = std::min(dev::kMaxRows, p->rows - r0);
-    const bool spec = K <= dev::kMaxSpecK;
-    int mul_terms = 0;  // coefficients that are neither 0 nor 1
-    for (int r = 0; r < R; ++r)
-      for (int j = 0; j < K; ++j) mul_terms += p->coef[size_t(r0 + r) * K + j] > 1u;
-    // The v_perm engine unless ECGPU_KERNEL / ecgpu_plan_set_kernel asks for the
-    // LDS nibble-table engine.  (Dense launches on the LDS engine were tried:
-    // an in-process interleaved A/B has v_perm 2.5 % faster on C4 decode
-    // {0,1,2,3} and even on RS(12,4) {0,1,2,3}, profiles/r02_engine_ab_inprocess.json.)
-    const bool use_lds = p->kind == ECGPU_KERNEL_LDS;
-    KernelFn vec_fn = spec ? spec_kernel(use_lds, K, R, unit_variant(p->coef, K, r0, R), p->nt) : generic_fn(R);
-    const int vec = 1;
-    // Both engines follow the cap rule; the LDS engine's allocation leaves room
-    // for its K * 128 B of tables (tools/encode_lab.hip --lds: RS(10,4) encode
-    // 1008 us uncapped, 902 at 3 per CU, v_perm 890).
-    const bool cap = cap_for(K, R, mul_terms);
-    const unsigned static_lds = use_lds && spec ? unsigned(K) * 32u * 4u : 0u;
-    uint64_t unit = 0, zero = 0;
-    if (spec)
-      for (int r = 0; r < R; ++r)
-        for (int j = 0; j < K; ++j) {
-          const uint32_t c = p->coef[size_t(r0 + r) * K + j];
-          if (c == 1) unit |= uint64_t(1) << (r * K + j);
-          if (c == 0) zero |= uint64_t(1) << (r * K + j);
-        }
-    for (int s0 = 0; s0 < p->stripes; s0 += kMaxGridY) {
-      const int ns = std::min(kMaxGridY, p->stripes - s0);
-      ApplyArgs a{};
-      a.qtab = p->d_q + size_t(r0) * K;
-      a.ptab = p->d_p3 + size_t(r0) * K * dev::kP3Words;
-      a.ntab = p->d_nib + size_t(r0) * K * 32;
-      a.src = p->d_src + size_t(s0) * K;
-      a.dst = p->d_dst + size_t(s0) * p->rows;
-      a.nvec = nvec;
-      a.size = p->size;
-      a.byte0 = byte0;
-      a.src_stride = K;
-      a.dst_stride = p->rows;
-      a.row0 = r0;
-      a.K = K;
-      a.R = R;
-      a.nt = p->nt;
-      a.unit_mask = unit;
-      a.zero_mask = zero;
-      if (nvec > 0) {
-        const int64_t per_block = int64_t(dev::kBlock) * vec;
-        const dim3 grid(unsigned((nvec + per_block - 1) / per_block), unsigned(ns));
-        const unsigned lds = cap ? residency_lds_bytes(p->device, K + R, static_lds) : 0u;
-        ECGPU_HIP(launch(vec_fn, grid, block, a, stream, lds));
-      }
-      if (byte0 < p->size) {
-        const dim3 grid(unsigned((p->size - byte0 + dev::kBlock - 1) / dev::kBlock), unsigned(ns));
-        ECGPU_HIP(launch(&dev::gf_apply_bytes, grid, block, a, stream));
-      }
-    }
-  }
-  return ECGPU_OK;
-}
-
 // ------------------------------------------------------ context pool ----
 
 hostsync::IdlePool<Ctx> g_pool;  // idle contexts (process lifetime)
@@ -629,6 +239,82 @@ int current_device() {
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess) d = 0;
   return d;
+}
+
+// ECGPU_DEVICES (or ecgpu_set_devices): the devices the synchronous
+// host-memory calls spread over.  Each calling thread is given one of them,
+// round-robin in the order threads make their first such call, and keeps it
+// -- so the reference client's byte-range encode pthreads
+// (client_main.cpp:1074-1164) each drive their own GPU and PCIe link.  Unset
+// (the default): the caller's current device, as before.  "all" = every
+// visible device; otherwise a comma-separated list (repeats allowed).
+std::mutex g_devices_mu;
+std::shared_ptr<const std::vector<int>> g_devices;  // null: unset
+std::atomic<uint64_t> g_device_rr{0};
+
+std::vector<int> parse_devices(const char* s, int visible) {
+  std::vector<int> out;
+  if (!s || !*s) return out;
+  if (std::strcmp(s, "all") == 0) {
+    for (int d = 0; d < visible; ++d) out.push_back(d);
+    return out;
+  }
+  const char* q = s;
+  while (*q) {
+    char* end = nullptr;
+    const long v = std::strtol(q, &end, 10);
+    if (end == q || v < 0 || v > 1023) return {};  // malformed: ignored as a whole
+    out.push_back(int(v));
+    q = end;
+    if (*q == ',') ++q;
+    else if (*q) return {};
+  }
+  return out;
+}
+
+std::shared_ptr<const std::vector<int>> device_list() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char* e = std::getenv("ECGPU_DEVICES");
+    if (!e || !*e) return;
+    int n = 0;
+    if (std::strcmp(e, "all") == 0 && (hipGetDeviceCount(&n) != hipSuccess || n <= 0)) {
+      (void)hipGetLastError();
+      n = 0;
+    }
+    auto v = std::make_shared<const std::vector<int>>(parse_devices(e, n));
+    std::lock_guard<std::mutex> lk(g_devices_mu);
+    if (!g_devices && !v->empty()) g_devices = v;
+  });
+  std::lock_guard<std::mutex> lk(g_devices_mu);
+  return g_devices;
+}
+
+// The device a synchronous call on host memory runs on: a forced
+// ECGPU_DEVICE, else this thread's device from the ECGPU_DEVICES list, else
+// the caller's current device.
+int host_call_device() {
+  if (knob(Knob::kDevice) >= 0) return knob(Knob::kDevice);
+  const auto list = device_list();
+  if (!list || list->empty()) return current_device();
+  thread_local std::shared_ptr<const std::vector<int>> t_list;
+  thread_local int t_dev = -1;
+  if (t_list != list) {
+    t_list = list;
+    t_dev = (*list)[size_t(g_device_rr.fetch_add(1, std::memory_order_relaxed) % list->size())];
+  }
+  return t_dev;
+}
+
+// A call naming device memory runs where that memory is (the current device,
+// as before: classify() rejects another device's buffers); an all-host call
+// takes host_call_device().
+int call_device(const std::vector<void*>& a, const std::vector<void*>& b) {
+  if (knob(Knob::kDevice) >= 0) return knob(Knob::kDevice);
+  const auto list = device_list();
+  if (!list || list->empty()) return current_device();
+  if (any_device_buffer(a) || any_device_buffer(b)) return current_device();
+  return host_call_device();
 }
 
 Ctx* acquire_ctx(int device, int* rc) {
@@ -646,7 +332,7 @@ Ctx* acquire_ctx(int device, int* rc) {
   // different contexts, unordered against each other.
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamDefault);
   if (e != hipSuccess) {
-    *rc = fail(ECGPU_ERR_HIP, std::string("hipStreamCreateWithFlags: ") + hipGetErrorString(e));
+    *rc = fail_hip(e, "hipStreamCreateWithFlags");
     delete c;
     return nullptr;
   }
@@ -658,7 +344,10 @@ void release_ctx(Ctx* c) { g_pool.release(c->device, c); }
 
 
 int ctx_plan(Ctx* c, int rows, int nsrc, const std::vector<uint32_t>& coef, int w, ecgpu_plan** out) {
-  PlanKey key{rows, nsrc, w, coef};
+  // the engine and store policy are part of the key: a knob switched between
+  // calls (an in-process A/B) must reach the next launch (plan_init reads them)
+  const int kind = knob(Knob::kKernel), nt = std::min(kStorePolicies - 1, std::max(0, knob(Knob::kNt)));
+  PlanKey key{rows, nsrc, w, kind, nt, coef};
   for (auto it = c->plans.begin(); it != c->plans.end(); ++it)
     if (it->first == key) {
       c->plans.splice(c->plans.begin(), c->plans, it);
@@ -1004,6 +693,23 @@ int map_buffers(const FusedOp& op, int64_t size, int device, bool inl, CallMap* 
   return ECGPU_OK;
 }
 
+// The call is about to write caller memory (a D2H or host copy into an
+// output, or a kernel writing an output in place): from here on a failure
+// cannot be completed on the CPU (cpu_fallback.hpp).  Also the test
+// injection's "after the first write" failure point.
+int caller_write_point(int device) {
+  note_caller_write();
+  return injected_failure(device, 1);
+}
+
+// Does a launch write some output in place (device memory, or pinned host
+// memory mapped for the kernel) rather than into staging?
+bool writes_in_place(const FusedOp& op, const CallMap& m) {
+  for (int r = 0; r < m.rows; ++r)
+    if (!m.staged[m.index(op.dsts[size_t(r)])]) return true;
+  return false;
+}
+
 int launch_and_sync(Ctx* c, const FusedOp& op, const CallMap& m, bool host_io) {
   if (int rc = launch_inline(op, m.sources(), m.outputs(op), m.size, c->stream, host_io)) return rc;
   ECGPU_HIP(hipStreamSynchronize(c->stream));
@@ -1020,7 +726,10 @@ int exec_zero_copy(Ctx* c, const FusedOp& op, CallMap& m) {
     if (m.staged[i]) m.devp[i] = c->zc + (next++) * m.slot;
   for (int j = 0; j < m.nsrc; ++j)
     if (m.staged[size_t(j)]) std::memcpy(m.devp[size_t(j)], op.srcs[size_t(j)], size_t(m.size));
+  if (writes_in_place(op, m))
+    if (int rc = caller_write_point(c->device)) return rc;
   if (int rc = launch_and_sync(c, op, m, /*host_io=*/true)) return rc;
+  if (int rc = caller_write_point(c->device)) return rc;
   for (int r = 0; r < m.rows; ++r) {
     const size_t i = m.index(op.dsts[size_t(r)]);
     if (m.staged[i]) std::memcpy(op.dsts[size_t(r)], m.devp[i], size_t(m.size));
@@ -1062,7 +771,10 @@ int exec_outputs_zero_copy(Ctx* c, const FusedOp& op, CallMap& m, bool* done) {
     }
   }
   if (int rc = copy_shards(true, c->stage, m.slot, staged_hp, size_t(m.size), c->stream)) return rc;
+  if (writes_in_place(op, m))
+    if (int rc = caller_write_point(c->device)) return rc;
   if (int rc = launch_and_sync(c, op, m, /*host_io=*/true)) return rc;
+  if (int rc = caller_write_point(c->device)) return rc;
   for (size_t i = 0; i < m.bufs.size(); ++i)
     if (m.staged[i] && is_out[i]) std::memcpy(m.bufs[i], m.devp[i], size_t(m.size));
   *done = true;
@@ -1105,6 +817,8 @@ int exec_staged(Ctx* c, const FusedOp& op, CallMap& m, bool inl) {
   std::vector<uint8_t*> dp = m.outputs(op);
   if (via_temp)
     for (int r = 0; r < rows; ++r) dp[size_t(r)] = c->stage + (m.nstage + size_t(r)) * slot;
+  if (writes_in_place(op, m))
+    if (int rc = caller_write_point(c->device)) return rc;
   if (nsrc == 0) {
     // Every output is identically zero (e.g. region multiply by 0 without
     // add, galois.cpp:447-451): nothing to read.
@@ -1139,9 +853,14 @@ int exec_staged(Ctx* c, const FusedOp& op, CallMap& m, bool inl) {
     }
     ECGPU_HIP(hipStreamSynchronize(c->stream));
     ECGPU_HIP(hipGetLastError());
+    if (!outs.empty())
+      if (int rc = caller_write_point(c->device)) return rc;
     for (const auto& o : outs) std::memcpy(o.second, c->bounce + (o.first - c->stage), size);
     return ECGPU_OK;
   }
+  // from here the D2H copies write the caller's outputs directly
+  if (!outs.empty())
+    if (int rc = caller_write_point(c->device)) return rc;
   // outputs in consecutive slots: one 2-D copy per evenly spaced run of host outputs
   bool consecutive = true;
   for (size_t i = 1; i < outs.size() && consecutive; ++i) consecutive = outs[i].first == outs[0].first + i * slot;
@@ -1161,7 +880,7 @@ int exec_staged(Ctx* c, const FusedOp& op, CallMap& m, bool inl) {
 // `device`: maps the buffers, then the cheapest staging mode for the host
 // ones (§8 of DESIGN.md; the thresholds are measured, see bounce_max / zc_max
 // / zc_out_max).
-int execute_on(const FusedOp& op, int64_t size, int device) {
+int execute_on_gpu(const FusedOp& op, int64_t size, int device) {
   CtxLease lease(device);
   if (!lease.c) return lease.rc;
   Ctx* c = lease.c;
@@ -1169,6 +888,7 @@ int execute_on(const FusedOp& op, int64_t size, int device) {
   const bool inl = inline_ok(op, size);
   CallMap m;
   if (int rc = map_buffers(op, size, device, inl, &m)) return rc;
+  if (int rc = injected_failure(device, 0)) return rc;
   if (inl && m.nstage > 0 && m.nstage * size_t(size) <= zc_max()) return exec_zero_copy(c, op, m);
   if (inl && m.nstage > 0 && m.nstage * m.slot > bounce_max()) {
     bool done = false;
@@ -1176,6 +896,43 @@ int execute_on(const FusedOp& op, int64_t size, int device) {
     if (done) return ECGPU_OK;
   }
   return exec_staged(c, op, m, inl);
+}
+
+// Is any buffer device (or managed) memory -- a call the CPU cannot complete?
+bool any_device_buffer(const std::vector<void*>& bufs) {
+  for (void* p : bufs) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+      (void)hipGetLastError();  // unregistered pageable memory (or no HIP at all)
+      continue;
+    }
+    if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) return true;
+  }
+  return false;
+}
+
+bool any_device_buffer(const FusedOp& op) {
+  return any_device_buffer(op.srcs) || any_device_buffer(op.dsts);
+}
+
+// execute_on_gpu under SURVEY §8b's failure contract (cpu_fallback.hpp): a
+// HIP error before any caller byte was written, on a call whose buffers are
+// all host memory, completes on the CPU (ECGPU_CPU_FALLBACK, default on);
+// a device marked lost by a sticky error sends such calls straight there.
+int execute_on(const FusedOp& op, int64_t size, int device, const char* call) {
+  trace_begin();
+  const bool fallback = fallback_enabled();
+  if (fallback && device_lost(device) && !any_device_buffer(op)) {
+    record_fallback(call, "device " + std::to_string(device) + " marked lost by an earlier HIP error");
+    cpu_apply(op, size);
+    return ECGPU_OK;
+  }
+  const int rc = execute_on_gpu(op, size, device);
+  if (rc != ECGPU_ERR_HIP || !fallback || caller_written() || any_device_buffer(op)) return rc;
+  record_fallback(call, "HIP error: " + t_err);
+  cpu_apply(op, size);
+  t_err = std::string(call) + ": completed on the CPU after a HIP error: " + t_err;
+  return ECGPU_OK;
 }
 
 // ------------------------------------------------------- split calls ----
@@ -1187,8 +944,9 @@ int execute_on(const FusedOp& op, int64_t size, int device) {
 // reference client's own split (encode_mul_thread, client_main.cpp:1074-1164)
 // done inside one call, and SURVEY §8e's "one huge stripe: contiguous byte
 // ranges of S/N" over the visible GPUs: each range crosses its own PCIe link.
-// ECGPU_SPLIT: 0 off (default), -1 one range per visible device, N > 0 N
-// ranges over the devices in turn (N > 1 on one GPU: N contexts on it);
+// ECGPU_SPLIT: 0 off (default), -1 one range per visible device (or per entry
+// of ECGPU_DEVICES), N > 0 N ranges over the devices in turn (N > 1 on one
+// GPU: N contexts on it; a forced ECGPU_DEVICE keeps them all there);
 // ranges are at least ECGPU_SPLIT_MIN_KIB.  Calls with a device buffer stay
 // whole (the buffer fixes the device).
 int split_ways(const FusedOp& op, int64_t size, int* ndev) {
@@ -1201,7 +959,9 @@ int split_ways(const FusedOp& op, int64_t size, int* ndev) {
   }
   *ndev = n;
   const int64_t min_bytes = int64_t(std::max(16, knob(Knob::kSplitMinKib))) << 10;
-  const int ways = int(std::min<int64_t>(v < 0 ? n : v, size / min_bytes));
+  const auto list = device_list();
+  const int per_device = list && !list->empty() ? int(list->size()) : n;  // -1: one range per listed / visible device
+  const int ways = int(std::min<int64_t>(v < 0 ? per_device : v, size / min_bytes));
   if (ways <= 1) return 1;
   auto on_host = [](const void* p) {
     hipPointerAttribute_t attr;
@@ -1228,14 +988,29 @@ FusedOp shifted(const FusedOp& op, int64_t off) {
   return s;
 }
 
-int execute_split(const FusedOp& op, int64_t size, int ways, int ndev) {
+int execute_split(const FusedOp& op, int64_t size, int ways, int ndev, const char* call) {
   const int64_t per = (size / ways) & ~int64_t(15);  // whole words at w = 16 / 32
   const int first = current_device();
+  // range i's device: a forced ECGPU_DEVICE keeps every range on it (N
+  // contexts there); an ECGPU_DEVICES list is walked from this thread's entry;
+  // otherwise every visible device in turn from the current one
+  const int forced = knob(Knob::kDevice);
+  const auto list = device_list();
+  size_t list_pos = 0;
+  if (forced < 0 && list && !list->empty()) {
+    const int mine = host_call_device();
+    list_pos = size_t(std::find(list->begin(), list->end(), mine) - list->begin()) % list->size();
+  }
+  auto range_device = [&](int i) {
+    if (forced >= 0) return forced;
+    if (list && !list->empty()) return (*list)[(list_pos + size_t(i)) % list->size()];
+    return (first + i) % ndev;
+  };
   std::vector<int> rc(size_t(ways), ECGPU_OK);
   std::vector<std::string> msg(static_cast<size_t>(ways));
   auto run = [&](int i) {
     const int64_t off = per * i, len = i + 1 < ways ? per : size - off;
-    rc[size_t(i)] = execute_on(shifted(op, off), len, (first + i) % ndev);
+    rc[size_t(i)] = execute_on(shifted(op, off), len, range_device(i), call);
     if (rc[size_t(i)]) msg[size_t(i)] = t_err;
   };
   std::vector<std::thread> workers;
@@ -1264,8 +1039,8 @@ int execute(const FusedOp& op, int64_t size, const char* call) {
   if (op.dsts.empty() || size <= 0) return ECGPU_OK;
   int ndev = 1;
   const int ways = split_ways(op, size, &ndev);
-  if (ways > 1) return execute_split(op, size, ways, ndev);
-  return execute_on(op, size, current_device());
+  if (ways > 1) return execute_split(op, size, ways, ndev, call);
+  return execute_on(op, size, call_device(op.srcs, op.dsts), call);
 }
 
 ECGPU_RT_END
@@ -1309,6 +1084,25 @@ ECGPU_API int ecgpu_plan_launch(ecgpu_plan* p, void* stream) {
 }
 
 ECGPU_API void ecgpu_plan_destroy(ecgpu_plan* p) { plan_free(p); }
+
+ECGPU_API int ecgpu_set_devices(int n, const int* devices) {
+  if (n < 0 || (n > 0 && !devices)) return fail(ECGPU_ERR_ARG, "ecgpu_set_devices: bad arguments");
+  for (int i = 0; i < n; ++i)
+    if (devices[i] < 0) return fail(ECGPU_ERR_ARG, "ecgpu_set_devices: negative device");
+  (void)device_list();  // the environment's list is read first, so this call overrides it
+  std::lock_guard<std::mutex> lk(g_devices_mu);
+  g_devices = n > 0 ? std::make_shared<const std::vector<int>>(devices, devices + n) : nullptr;
+  return ECGPU_OK;
+}
+
+ECGPU_API int ecgpu_get_devices(int* out, int cap) {
+  const auto list = device_list();
+  const int n = list ? int(list->size()) : 0;
+  for (int i = 0; i < n && i < cap && out; ++i) out[i] = (*list)[size_t(i)];
+  return n;
+}
+
+ECGPU_API int ecgpu_call_device(void) { return host_call_device(); }
 
 ECGPU_API int ecgpu_device_pci_bus_id(int device, char* buf, int len) {
   if (!buf || len < 13) return fail(ECGPU_ERR_ARG, "ecgpu_device_pci_bus_id: buffer of >= 13 bytes required");

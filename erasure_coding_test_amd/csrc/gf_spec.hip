@@ -1,5 +1,5 @@
-// gf_spec.hip -- one R's share of the specialised kernel table (gf_spec.hpp).
-// Built four times: -DECGPU_SPEC_R=1..4.
+// gf_spec.hip -- one R's share of the specialised w = 8 kernel table
+// (gf_spec.hpp).  Built four times: -DECGPU_SPEC_R=1..4.
 #include <hip/hip_runtime.h>
 
 #include "gf_spec.hpp"
@@ -38,25 +38,6 @@ struct Row {
   static constexpr SpecKernelFn lds = &dev::gf_apply_lds<K, kR>;
 };
 
-template <int K>
-constexpr SpecKernelFn wide_unit_fn() {
-  if constexpr (kR >= 2) return &dev::gf_apply_wide_pipe<K, kR, dev::kPipeW32Unit>;
-  else return nullptr;  // the unit form needs a row besides the unit row
-}
-
-template <int K>
-struct WidePipe {
-  static constexpr SpecKernelFn fn[3] = {&dev::gf_apply_wide_pipe<K, kR, dev::kPipeW32>, wide_unit_fn<K>(),
-                                         &dev::gf_apply_wide_pipe<K, kR, dev::kPipeW16>};
-};
-
-template <int... Ks>
-SpecKernelFn pick_wide_pipe(int K, int mode) {
-  SpecKernelFn out = nullptr;
-  ((K == Ks ? (out = WidePipe<Ks>::fn[mode], 0) : 0), ...);
-  return out;
-}
-
 template <int... Ks>
 SpecKernelFn pick(bool lds, int K, int u, int store_pol) {
   SpecKernelFn out = nullptr;
@@ -83,11 +64,6 @@ SpecKernelFn ECGPU_CAT(spec_kernel_r, ECGPU_SPEC_R)(bool lds, int K, int unit_va
 InlineKernelFn ECGPU_CAT(inline_kernel_r, ECGPU_SPEC_R)(int K, int unit_variant, bool zc) {
   if (unit_variant < 0 || unit_variant > 4) return nullptr;
   return pick_inl<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>(K, unit_variant, zc);
-}
-
-SpecKernelFn ECGPU_CAT(wide_pipe_kernel_r, ECGPU_SPEC_R)(int K, int mode) {
-  if (mode < 0 || mode > 2) return nullptr;
-  return pick_wide_pipe<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16>(K, mode);
 }
 
 }  // namespace ecgpu

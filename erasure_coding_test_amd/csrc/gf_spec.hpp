@@ -30,24 +30,6 @@ InlineKernelFn inline_kernel_r2(int K, int unit_variant, bool zc);
 InlineKernelFn inline_kernel_r3(int K, int unit_variant, bool zc);
 InlineKernelFn inline_kernel_r4(int K, int unit_variant, bool zc);
 
-// gf_apply_wide_pipe<K, R, mode> (w = 16 / 32 nibble tables, pipelined
-// loads; mode: dev::WidePipeMode); nullptr if K is outside 1..kMaxSpecK or
-// the mode needs more rows (the unit form: R >= 2).
-SpecKernelFn wide_pipe_kernel_r1(int K, int mode);
-SpecKernelFn wide_pipe_kernel_r2(int K, int mode);
-SpecKernelFn wide_pipe_kernel_r3(int K, int mode);
-SpecKernelFn wide_pipe_kernel_r4(int K, int mode);
-
-inline SpecKernelFn wide_pipe_kernel(int K, int R, int mode) {
-  switch (R) {
-    case 1: return wide_pipe_kernel_r1(K, mode);
-    case 2: return wide_pipe_kernel_r2(K, mode);
-    case 3: return wide_pipe_kernel_r3(K, mode);
-    case 4: return wide_pipe_kernel_r4(K, mode);
-    default: return nullptr;
-  }
-}
-
 inline InlineKernelFn inline_kernel(int K, int R, int unit_variant, bool zc) {
   switch (R) {
     case 1: return inline_kernel_r1(K, unit_variant, zc);

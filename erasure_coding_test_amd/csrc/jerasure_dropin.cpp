@@ -6,8 +6,11 @@
 // ECX datanode (ecx_datanode_main.cpp:714, :724, :1391) link this library in
 // place of src/erasure_coding/*.cpp.  The w = 8 hot path -- matrix encode,
 // decode, dot product, region multiply / XOR, parity, RAID-6 -- runs on the
-// MI355X through include/ecgpu.h; a GPU failure takes the reference's own
-// failure channel (see gpu_fatal), never a silent CPU fallback.  The w = 16 / 32 region and matrix calls run
+// MI355X through include/ecgpu.h.  A HIP failure before any caller byte was
+// written, on host buffers, is completed on the CPU inside libecgpu (SURVEY
+// §8b "no new failure modes", cpu_fallback.hpp; counted, logged once); any
+// other GPU failure takes the reference's own failure channel (gpu_fatal).
+// The w = 16 / 32 region and matrix calls run
 // on the MI355X too (wide-word kernels) when the size is a whole number of
 // words -- the reference's own precondition (jerasure.h: size a multiple of
 // sizeof(long)); a ragged size, where the reference reads and writes past the
@@ -31,8 +34,10 @@
 
 namespace {
 
-// A GPU failure surfaces through the reference's OWN failure channels, never
-// a silent CPU fallback: calls that return a status report it there
+// A GPU failure libecgpu could not complete on the CPU -- the fallback is off
+// (ECGPU_CPU_FALLBACK=0), a buffer is device memory, or the call had already
+// written caller memory -- surfaces through the reference's OWN failure
+// channels: calls that return a status report it there
 // (jerasure_matrix_decode returns -1, which the client already handles,
 // client_main.cpp:2118-2124); void calls print a message and exit(1), the
 // reference's convention for unrecoverable conditions (galois.cpp:330-334,
@@ -41,11 +46,17 @@ namespace {
 // overlapping another region of the call, buffer_contract.hpp) take the same
 // channel: the reference's bytes for them depend on its loop order, and a
 // silently different answer would be worse than the reference's own exit.
+const char* fallback_note() {
+  int on = 1;
+  return ecgpu_get_knob("ECGPU_CPU_FALLBACK", &on) == ECGPU_OK && on == 0 ? " [CPU fallback off: ECGPU_CPU_FALLBACK=0]"
+                                                                          : "";
+}
+
 [[noreturn]] void gpu_fatal(const char* fn, int rc) {
   if (rc == ECGPU_ERR_ARG)
     std::fprintf(stderr, "%s: arguments rejected (%d): %s\n", fn, rc, ecgpu_last_error());
   else
-    std::fprintf(stderr, "%s: MI355X path failed (%d): %s\n", fn, rc, ecgpu_last_error());
+    std::fprintf(stderr, "%s: MI355X path failed (%d): %s%s\n", fn, rc, ecgpu_last_error(), fallback_note());
   std::exit(1);
 }
 
@@ -167,8 +178,9 @@ int jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int
   const int rc = ecgpu_jerasure_matrix_decode(k, m, w, matrix, row_k_ones, erasures, data_ptrs, coding_ptrs, size);
   if (rc == ECGPU_ERR) return -1;
   if (rc != ECGPU_OK) {  // the reference's failure result, with the reason on stderr
-    std::fprintf(stderr, "jerasure_matrix_decode: %s (%d): %s\n",
-                 rc == ECGPU_ERR_ARG ? "arguments rejected" : "MI355X path failed", rc, ecgpu_last_error());
+    std::fprintf(stderr, "jerasure_matrix_decode: %s (%d): %s%s\n",
+                 rc == ECGPU_ERR_ARG ? "arguments rejected" : "MI355X path failed", rc, ecgpu_last_error(),
+                 rc == ECGPU_ERR_ARG ? "" : fallback_note());
     return -1;
   }
   return 0;

@@ -34,8 +34,10 @@ double g_stats[3] = {0, 0, 0};
 inline char* dev_ptr(int id, int k, char** data, char** coding) { return id < k ? data[id] : coding[id - k]; }
 }  // namespace
 
-// GPU packet-coding calls: a failure is a message + exit(1) (the reference's
-// convention for unrecoverable conditions), never a silent CPU fallback.
+// GPU packet-coding calls: a failure libecgpu could not complete on the CPU
+// (cpu_fallback.hpp: fallback off, device memory, or caller memory already
+// written) is a message + exit(1), the reference's convention for
+// unrecoverable conditions.
 void gpu_check(const char* fn, int rc) {
   if (rc == ECGPU_OK) return;
   std::fprintf(stderr, "%s: MI355X path failed (%d): %s\n", fn, rc, ecgpu_last_error());

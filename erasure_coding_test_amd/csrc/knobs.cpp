@@ -13,7 +13,7 @@
 
 namespace ecgpu {
 namespace __attribute__((visibility("hidden"))) rt {
-int fail(int code, const std::string& msg);  // ecgpu_runtime.hip
+int fail(int code, const std::string& msg);  // capi_host.cpp
 }
 
 namespace {
@@ -51,6 +51,8 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_SPLIT", "split", 0},
     {"ECGPU_SPLIT_MIN_KIB", "split_min_kib", 1024},
     {nullptr, "test_d2h_delay_us", 0},
+    {"ECGPU_CPU_FALLBACK", "cpu_fallback", 1},
+    {"ECGPU_TEST_INJECT_HIP", "test_inject_hip", 0},
 };
 
 constexpr int kUnset = INT_MIN;
@@ -124,8 +126,9 @@ ECGPU_API int ecgpu_reset_knob(const char* name) {
 }
 
 ECGPU_API int ecgpu_get_knob(const char* name, int* value) {
+  if (!value) return ecgpu::rt::fail(ECGPU_ERR_ARG, "ecgpu_get_knob: value is NULL");
   ecgpu::Knob k;
-  if (!value || !ecgpu::knob_by_name(name, &k))
+  if (!ecgpu::knob_by_name(name, &k))
     return ecgpu::rt::fail(ECGPU_ERR_ARG, std::string("ecgpu_get_knob: unknown knob ") + (name ? name : "(null)"));
   *value = ecgpu::knob(k);
   return ECGPU_OK;

@@ -41,6 +41,10 @@ enum class Knob : int {
   kSplitMinKib,     // ECGPU_SPLIT_MIN_KIB: smallest range of a split call
   kTestD2hDelayUs,  // tests only, set with ecgpu_set_knob (no environment variable): the D2H
                     // worker sleeps this long before issuing a job (widens a race window)
+  kCpuFallback,     // ECGPU_CPU_FALLBACK: a synchronous host-memory call that hits a HIP error before
+                    // writing caller memory completes on the CPU (cpu_fallback.hpp), 1 on (default), 0 off
+  kTestInjectHip,   // ECGPU_TEST_INJECT_HIP (tests only): synchronous calls fail with ECGPU_ERR_HIP, 1 before
+                    // the first launch, 2 the same and the device marked lost, 3 after writing caller memory
   kCount
 };
 

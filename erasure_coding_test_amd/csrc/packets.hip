@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "buffer_contract.hpp"
+#include "cpu_fallback.hpp"
 #include "ecgpu.h"
 #include "gf_host.hpp"
 #include "matrix_host.hpp"
@@ -60,6 +61,10 @@ bool unit_packet_map(const uint32_t* m, int nsrc) {
   return true;
 }
 
+int execute_packets_gpu(const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride, int64_t ps,
+                        int device, const std::vector<int>& slots, const std::vector<int64_t>& extent,
+                        const std::vector<char>& is_out);
+
 // Slot s's packet row r of super-packet sp is ptrs[s] + sp * spstride + r * ps.
 int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride, int64_t ps,
                     const char* call) {
@@ -84,13 +89,38 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
     if (int rc = touch(k, false)) return rc;
   for (void* k : op.dsts)
     if (int rc = touch(k, true)) return rc;
-  const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
   std::vector<int64_t> extent(ptrs.size(), 0);
   for (int sl : slots) extent[size_t(sl)] = (nsp - 1) * spstride + (maxrow[size_t(sl)] + 1) * ps;
   // identical or disjoint device buffers, checked before anything touches the GPU
   if (int rc = check_slot_buffers(call, ptrs, slots, extent, is_out)) return rc;
   add_stats(op);
-  const int device = current_device();
+  std::vector<void*> slot_ptrs;
+  for (int sl : slots) slot_ptrs.push_back(ptrs[size_t(sl)]);
+  const int device = call_device(slot_ptrs, {});
+  // SURVEY §8b's failure contract, as for the w = 8 calls (cpu_fallback.hpp):
+  // host-memory calls complete on the CPU after a HIP error that came before
+  // any caller byte was written, or at once on a device marked lost
+  trace_begin();
+  const bool fallback = fallback_enabled();
+  if (fallback && device_lost(device) && !any_device_buffer(slot_ptrs)) {
+    record_fallback(call, "device " + std::to_string(device) + " marked lost by an earlier HIP error");
+    cpu_apply_packets(op, ptrs, nsp, spstride, ps);
+    return ECGPU_OK;
+  }
+  const int rc = execute_packets_gpu(op, ptrs, nsp, spstride, ps, device, slots, extent, is_out);
+  if (rc != ECGPU_ERR_HIP || !fallback || caller_written() || any_device_buffer(slot_ptrs)) return rc;
+  record_fallback(call, "HIP error: " + t_err);
+  cpu_apply_packets(op, ptrs, nsp, spstride, ps);
+  t_err = std::string(call) + ": completed on the CPU after a HIP error: " + t_err;
+  return ECGPU_OK;
+}
+
+// The GPU part of execute_packets: staging, one launch per 32 output rows,
+// the copies back.
+int execute_packets_gpu(const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride, int64_t ps,
+                        int device, const std::vector<int>& slots, const std::vector<int64_t>& extent,
+                        const std::vector<char>& is_out) {
+  const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
   CtxLease lease(device);
   if (!lease.c) return lease.rc;
   Ctx* c = lease.c;
@@ -113,6 +143,7 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
       off += (size_t(extent[size_t(sl)]) + 255) & ~size_t(255);
     }
   }
+  if (int rc = injected_failure(device, 0)) return rc;
   const size_t temp_off = off;
   if (via_temp) off += size_t(rows) * size_t(nsp * ps + 255 & ~int64_t(255));
   const size_t tab_off = off;
@@ -222,6 +253,8 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
       ECGPU_HIP(hipMemcpy2DAsync(real, size_t(nsp > 1 ? spstride : ps), db[size_t(r)], size_t(ps), size_t(ps),
                                  size_t(nsp), hipMemcpyDeviceToDevice, c->stream));
     }
+  note_caller_write();  // the launches above wrote device slots in place; the copies below write host ones
+  if (int rc = injected_failure(device, 1)) return rc;
   for (int sl : slots)
     if (staged[size_t(sl)] && is_out[size_t(sl)])
       ECGPU_HIP(hipMemcpyAsync(ptrs[size_t(sl)], base[size_t(sl)], size_t(extent[size_t(sl)]), hipMemcpyDeviceToHost,

@@ -64,11 +64,15 @@ ECGPU_RT_BEGIN
 extern thread_local std::string t_err;  // ecgpu_last_error()
 int fail(int code, const std::string& msg);  // knobs: knobs.hpp
 
-#define ECGPU_HIP(expr)                                                                          \
-  do {                                                                                           \
-    hipError_t e_ = (expr);                                                                      \
-    if (e_ != hipSuccess)                                                                        \
-      return ::ecgpu::rt::fail(ECGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+// A HIP failure: ECGPU_ERR_HIP with the message; an error that leaves the
+// device's context unusable (sticky: a kernel fault, a lost or missing
+// device) also marks the current device lost (cpu_fallback.hpp).
+int fail_hip(hipError_t e, const char* what);
+
+#define ECGPU_HIP(expr)                                 \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return ::ecgpu::rt::fail_hip(e_, #expr); \
   } while (0)
 
 struct DeviceGuard {
@@ -84,9 +88,38 @@ struct DeviceGuard {
 };
 
 int current_device();
+// The device a synchronous call on these buffers runs on (ECGPU_DEVICE,
+// ECGPU_DEVICES, or the current device; ecgpu_runtime.hip).
+int call_device(const std::vector<void*>& a, const std::vector<void*>& b);
+
+// ---- kernel launches -----------------------------------------------------------
+using KernelFn = void (*)(ecgpu::dev::ApplyArgs);
+
+inline hipError_t launch(KernelFn fn, dim3 grid, dim3 block, ecgpu::dev::ApplyArgs& a, hipStream_t s,
+                         unsigned lds_bytes = 0) {
+  void* args[] = {&a};
+  return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, block, args, lds_bytes, s);
+}
+
+// dispatch_w8.hip: which compile-time unit structure holds exactly for rows
+// [r0, r0 + R) (gf_kernels_w8.hpp UnitMask index), the residency cap's
+// dynamic LDS bytes for a launch streaming `streams` shards per lane, and
+// whether a launch takes the cap
+int unit_variant(const std::vector<uint32_t>& coef, int K, int r0, int R);
+unsigned residency_lds_bytes(int device, int streams, unsigned static_bytes = 0);
+bool cap_for(int K, int R, int mul_terms);
 
 // ---- plans --------------------------------------------------------------------
 void plan_free(ecgpu_plan* p);
+// one asynchronous upload of a plan's coefficient tables (ecgpu_runtime.hip);
+// launches wait for it through plan_wait_tables
+int plan_upload_tables(ecgpu_plan* p, std::vector<uint8_t>&& host);
+int plan_wait_tables(ecgpu_plan* p, hipStream_t stream);
+// the width-specific halves of plan_init / plan_launch (dispatch_w8.hip,
+// dispatch_wide.hip); p->coef is sized rows x nsrc
+int plan_init_w8(ecgpu_plan* p, const int* coefs);
+int plan_init_wide(ecgpu_plan* p, const int* coefs);
+int plan_launch_wide(ecgpu_plan* p, hipStream_t stream);
 int plan_init(ecgpu_plan* p, int rows, int nsrc, const int* coefs, int device, int w = 8);
 // With a stream the pointer tables are uploaded asynchronously on it; unless
 // `keep_alive` (the caller keeps src/dst alive until it synchronises the
@@ -97,9 +130,11 @@ int plan_launch(ecgpu_plan* p, hipStream_t stream);
 
 // ---- contexts of the synchronous calls ----------------------------------------
 struct PlanKey {
-  int rows, nsrc, w;
+  int rows, nsrc, w, kind, nt;  // kind / nt: the engine and store-policy knobs the plan was made under
   std::vector<uint32_t> coef;
-  bool operator==(const PlanKey& o) const { return rows == o.rows && nsrc == o.nsrc && w == o.w && coef == o.coef; }
+  bool operator==(const PlanKey& o) const {
+    return rows == o.rows && nsrc == o.nsrc && w == o.w && kind == o.kind && nt == o.nt && coef == o.coef;
+  }
 };
 
 struct Ctx {
@@ -146,5 +181,8 @@ int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, cons
 // Runs a fused op synchronously; `call` names the entry point in errors
 // (e.g. a buffer-contract rejection, buffer_contract.hpp).
 int execute(const FusedOp& op, int64_t size, const char* call = "ecgpu");
+// Is any of these buffers device (or managed) memory -- a call the CPU
+// fallback cannot complete (cpu_fallback.hpp)?
+bool any_device_buffer(const std::vector<void*>& bufs);
 
 ECGPU_RT_END

@@ -18,9 +18,14 @@
  * star), 16 or 32 (wide-word kernels; size a whole number of w/8-byte words,
  * else ECGPU_ERR_ARG) and so do the w16/w32 region functions.  These accept host OR device pointers
  * (classified per buffer; host buffers are staged through HBM) and are
- * synchronous: results are valid on return, like the reference.  They never
- * fall back to a CPU path; a HIP failure returns ECGPU_ERR_HIP (or, through
- * the void-returning drop-in names, exits with a message).  Buffers of one
+ * synchronous: results are valid on return, like the reference.  A HIP
+ * failure on a call whose buffers are all host memory, before any byte of
+ * them was written, completes on the CPU (no new failure modes;
+ * counted by ecgpu_fallback_count, the first one logged on stderr) unless the
+ * ECGPU_CPU_FALLBACK knob is 0; any other HIP failure returns ECGPU_ERR_HIP
+ * (through the void-returning drop-in names: exits with a message).  The
+ * Python package turns the fallback off unless the environment sets the
+ * knob, and the bench and tests assert the count is 0.  Buffers of one
  * call are identical or disjoint: a written region that partially overlaps
  * another region of the call returns ECGPU_ERR_ARG before anything runs
  * (see ecgpu_plan_check_buffers).
@@ -57,8 +62,9 @@ enum { ECGPU_KERNEL_PERM = 0, ECGPU_KERNEL_LDS = 1 };
 /* ---------------------------------------------------------------- misc -- */
 ECGPU_API const char* ecgpu_version(void);
 /* Content IDs of the built library (16 hex digits): what = 0 the whole
- * library, 1 the coding kernels and their dispatch (the identity a rocprofv3
- * PMC record of a launch is valid for). */
+ * library, 1 the w = 8 kernels and their dispatch (the identity a rocprofv3
+ * PMC record of the bench's launches is valid for), 2 the w = 16 / 32
+ * kernels, 3 the GF(2) packet kernels. */
 ECGPU_API const char* ecgpu_build_id(int what);
 ECGPU_API const char* ecgpu_last_error(void);         /* thread-local message */
 /* Tuning / A-B switches (knobs.hpp lists them: the residency cap, engines,
@@ -71,6 +77,28 @@ ECGPU_API int ecgpu_set_knob(const char* name, int value);
 ECGPU_API int ecgpu_reset_knob(const char* name);
 ECGPU_API int ecgpu_get_knob(const char* name, int* value);
 ECGPU_API void ecgpu_free(void* p);                    /* == free()           */
+/* SURVEY §8b failure contract: synchronous calls completed on the CPU after a
+ * HIP error (process total), and whether a sticky HIP error (kernel fault,
+ * lost device) marked `device` unusable -- with ECGPU_CPU_FALLBACK on, later
+ * host-memory calls on it run on the CPU without touching it. */
+ECGPU_API int64_t ecgpu_fallback_count(void);
+ECGPU_API int ecgpu_device_lost(int device);
+/* The devices synchronous host-memory calls spread over (default: unset, the
+ * caller's current device).  Each calling thread is given one entry,
+ * round-robin in the order threads make their first such call, and keeps it,
+ * so concurrent callers (the reference client's byte-range encode pthreads,
+ * client_main.cpp:1074-1164) each drive their own GPU.  Also read from
+ * ECGPU_DEVICES ("all" or "0,1,2,..."; repeats allowed) at first use; n = 0
+ * unsets.  A forced ECGPU_DEVICE wins; calls naming device memory run on the
+ * current device.  get_devices returns the list's length (0 if unset) and
+ * copies up to cap entries; call_device is the device this thread's next
+ * host-memory call runs on. */
+ECGPU_API int ecgpu_set_devices(int n, const int* devices);
+ECGPU_API int ecgpu_get_devices(int* out, int cap);
+ECGPU_API int ecgpu_call_device(void);
+/* Specialised w = 8 column launches so far per engine (kind =
+ * ECGPU_KERNEL_PERM / ECGPU_KERNEL_LDS): which engine a knob setting reached. */
+ECGPU_API int64_t ecgpu_engine_launches(int kind);
 
 /* ------------------------------------- GF(2^w) scalar ops (host only) --- */
 ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w); /* galois.cpp:322-360 */

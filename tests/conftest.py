@@ -14,6 +14,12 @@ for p in (ROOT, TESTS):
 GOLDEN_DIR = os.path.join(TESTS, "golden")
 REFERENCE_ROOT = "/root/reference"
 
+# No test result may come from the drop-in's CPU fallback (SURVEY §8b,
+# csrc/cpu_fallback.hpp): off for this process and every process a test
+# starts, unless the test sets it itself (tests/test_cpu_fallback.py).
+os.environ["ECGPU_CPU_FALLBACK"] = "0"
+os.environ.pop("ECGPU_TEST_INJECT_HIP", None)
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box with -m gpu)")
@@ -75,3 +81,13 @@ def knobs():
 
     yield Knobs()
     N.reset_knob(None)
+
+
+@pytest.fixture(autouse=True)
+def _no_cpu_fallback():
+    """Every test ends with ecgpu_fallback_count() == 0 in this process: a GPU
+    result that silently came from the CPU would void the parity claims."""
+    yield
+    N = sys.modules.get("erasure_coding_test_amd._native")
+    if N is not None:
+        assert N.fallback_count() == 0, "a synchronous call completed on the CPU fallback inside the test session"

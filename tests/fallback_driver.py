@@ -1,0 +1,283 @@
+"""Subprocess driver of the CPU-fallback tests (tests/test_cpu_fallback.py):
+the reference's own callers' call sequences through libjerasure_amd.so's
+C++-mangled names, checked against golden fixtures and the reference built
+here (oracle/_ref, as the checker).
+
+    python tests/fallback_driver.py client|ecx|surface
+
+Run with ECGPU_TEST_INJECT_HIP / ECGPU_CPU_FALLBACK in the environment; prints
+one JSON line {"scenario", "checked", "mismatches", "fallbacks", "lost"} and
+exits 0 when every output matched (the drop-in itself exits 1 where a call
+cannot complete).  No torch: the drop-in is loaded the way an unchanged C++
+caller loads it.
+
+* client -- the reference client's calls (client_main.cpp:1060, :2118,
+  :1670): reed_sol_vandermonde_coding_matrix, jerasure_matrix_encode on C1-C3
+  golden stripes at 4096 / 4099 / 1000 B, every golden inconsistent decode
+  (return code and bytes), and a C3 4 MiB encode + decode{0,1,2,3} round trip
+  on one malloc'd stripe buffer (the staged large-call path).
+* ecx -- the ECX datanode's per-block sequence (ecx_datanode_main.cpp:
+  699-734): RS(3,3) blocks of 349,525 B arriving one source at a time, each
+  parity block memcpy'd / galois_region_xor'd / galois_w08_region_multiply'd
+  with init[], against the reference's encode of the same blocks; plus the
+  golden region-op cases.
+* surface -- the rest of the header surface on the fallback: w = 16 / 32
+  region multiplies and matrix encode, dot products, bit-matrix and schedule
+  encode, RAID-6, against the reference (-fno-strict-aliasing build for w = 16).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+TESTS = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(TESTS)
+sys.path.insert(0, TESTS)
+from ecdata import CONFIGS, fnv1a64, shard_seed, splitmix_bytes  # noqa: E402
+
+LIB = os.path.join(ROOT, "erasure_coding_test_amd", "lib")
+REF = os.path.join(ROOT, "oracle", "_ref")
+I = ctypes.c_int
+P = ctypes.c_void_p
+PP = ctypes.POINTER(ctypes.c_void_p)
+IP = ctypes.POINTER(ctypes.c_int)
+
+# mangled names (include/dropin/*.h)
+SIGS = {
+    "vdm": ("_Z34reed_sol_vandermonde_coding_matrixiii", P, [I, I, I]),
+    "encode": ("_Z22jerasure_matrix_encodeiiiPiPPcS1_i", None, [I, I, I, IP, PP, PP, I]),
+    "decode": ("_Z22jerasure_matrix_decodeiiiPiiS_PPcS1_i", I, [I, I, I, IP, I, IP, PP, PP, I]),
+    "dotprod": ("_Z23jerasure_matrix_dotprodiiPiS_iPPcS1_i", None, [I, I, IP, IP, I, PP, PP, I]),
+    "rmul8": ("_Z26galois_w08_region_multiplyPciiS_i", None, [P, I, I, P, I]),
+    "rmul16": ("_Z26galois_w16_region_multiplyPciiS_i", None, [P, I, I, P, I]),
+    "rmul32": ("_Z26galois_w32_region_multiplyPciiS_i", None, [P, I, I, P, I]),
+    "rxor": ("_Z17galois_region_xorPcS_S_i", None, [P, P, P, I]),
+    "to_bitmatrix": ("_Z28jerasure_matrix_to_bitmatrixiiiPi", P, [I, I, I, IP]),
+    "bm_encode": ("_Z25jerasure_bitmatrix_encodeiiiPiPPcS1_ii", None, [I, I, I, IP, PP, PP, I, I]),
+    "smart_sched": ("_Z36jerasure_smart_bitmatrix_to_scheduleiiiPi", P, [I, I, I, IP]),
+    "sched_encode": ("_Z24jerasure_schedule_encodeiiiPPiPPcS2_ii", None, [I, I, I, P, PP, PP, I, I]),
+    "r6": ("_Z18reed_sol_r6_encodeiiPPcS0_i", I, [I, I, PP, PP, I]),
+}
+
+
+def bind(path):
+    L = ctypes.CDLL(path)
+    f = {}
+    for key, (name, res, args) in SIGS.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+        f[key] = fn
+    return f
+
+
+def ptrs(bufs):
+    return (P * len(bufs))(*[b.ctypes.data for b in bufs])
+
+
+def ints(v):
+    return (I * len(v))(*v)
+
+
+def matrix(f, k, m, w=8):
+    p = f["vdm"](k, m, w)
+    return list((I * (k * m)).from_address(p))
+
+
+def shards(cfg, stripe, count, size, first=0, pad=16):
+    out = []
+    for s in range(count):
+        b = np.zeros(size + pad, np.uint8)
+        b[:size] = splitmix_bytes(size, shard_seed(cfg, stripe, first + s))
+        out.append(b)
+    return out
+
+
+class Run:
+    def __init__(self, name):
+        self.name, self.checked, self.mismatches = name, 0, []
+
+    def check(self, ok, what):
+        self.checked += 1
+        if not ok:
+            self.mismatches.append(what)
+
+
+def client(d, golden, run):
+    for cfg in (1, 2, 3):
+        k, m = CONFIGS[cfg]["k"], CONFIGS[cfg]["m"]
+        M = matrix(d, k, m)
+        for size in (4096, 4099, 1000):
+            for stripe in range(2):
+                data = shards(cfg, stripe, k, size)
+                coding = [np.zeros(size + 16, np.uint8) for _ in range(m)]
+                d["encode"](k, m, 8, ints(M), ptrs(data), ptrs(coding), size)
+                run.check([fnv1a64(c[:size]) for c in coding] == golden["encode_small"][f"C{cfg}:{size}:{stripe}"],
+                          f"encode C{cfg} {size} stripe {stripe}")
+    mats = {}
+    for case in golden["decode_inconsistent"]:
+        k, m, cfg, size = case["k"], case["m"], case["cfg"], case["size"]
+        if (k, m) not in mats:
+            mats[(k, m)] = matrix(d, k, m)
+        bufs = shards(cfg, 7, k, size) + shards(cfg, 7, m, size, first=k)
+        rc = d["decode"](k, m, 8, ints(mats[(k, m)]), case["row_k_ones"], ints(case["erasures"] + [-1]),
+                         ptrs(bufs[:k]), ptrs(bufs[k:]), size)
+        run.check(rc == case["rc"], f"decode rc {case['erasures']}")
+        if rc == 0:
+            run.check([fnv1a64(b[:size]) for b in bufs] == case["digests"],
+                      f"decode bytes {case['cfg']} {case['erasures']} rko {case['row_k_ones']}")
+    # one client stripe buffer, C3 at 4 MiB: the large staged path, then a round trip
+    k, m, size = 10, 4, 4 << 20
+    M = matrix(d, k, m)
+    slab = np.zeros((k + m) * size, np.uint8)
+    sh = [slab[i * size:(i + 1) * size] for i in range(k + m)]
+    for i in range(k):
+        sh[i][:] = splitmix_bytes(size, shard_seed(3, 0, i))
+    d["encode"](k, m, 8, ints(M), ptrs(sh[:k]), ptrs(sh[k:]), size)
+    run.check([fnv1a64(c) for c in sh[k:]] == golden["full_size"]["C3"]["coding"], "C3 4 MiB encode digests")
+    keep = [s.copy() for s in sh[:4]]
+    for s in sh[:4]:
+        s[:] = 0xEE
+    rc = d["decode"](k, m, 8, ints(M), 0, ints([0, 1, 2, 3, -1]), ptrs(sh[:k]), ptrs(sh[k:]), size)
+    run.check(rc == 0 and all(np.array_equal(a, b) for a, b in zip(sh[:4], keep)), "C3 4 MiB decode{0,1,2,3}")
+
+
+def ecx(d, ref, golden, run):
+    k, m, bs = 3, 3, (1 << 20) // 3  # the reference client's EC_K / EC_M; 349,525 B blocks
+    M = matrix(d, k, m)
+    blocks = shards(40, 0, k, bs)
+    acc = [np.zeros(bs + 8, np.uint8) for _ in range(m)]
+    init = [0] * m
+    for j in range(k):  # ecx_datanode_main.cpp:699-734, block j of source j
+        for i in range(m):
+            c = M[i * k + j]
+            if c == 1:
+                if not init[i]:
+                    acc[i][:bs] = blocks[j][:bs]
+                    init[i] = 1
+                else:
+                    d["rxor"](blocks[j].ctypes.data, acc[i].ctypes.data, acc[i].ctypes.data, bs)
+            if c not in (0, 1):
+                d["rmul8"](blocks[j].ctypes.data, c, bs, acc[i].ctypes.data, init[i])
+                init[i] = 1
+    want = [np.zeros(bs + 16, np.uint8) for _ in range(m)]
+    ref["encode"](k, m, 8, ints(M), ptrs(blocks), ptrs(want), bs)
+    for i in range(m):
+        run.check(np.array_equal(acc[i][:bs], want[i][:bs]), f"ECX parity block {i}")
+    for case in golden["region_multiply"]:
+        size, t = case["size"], case["seed_stripe"]
+        src = shards(10, t, 1, size)[0]
+        dst = shards(10, t, 1, size, first=1)[0]
+        if case["mode"] == "r2":
+            d["rmul8"](src.ctypes.data, case["multby"], size, dst.ctypes.data, case["add"])
+            out = dst
+        else:
+            d["rmul8"](src.ctypes.data, case["multby"], size, None, case["add"])
+            out = src
+        run.check(fnv1a64(out[:size]) == case["digest"], f"region multiply {case}")
+    for case in golden["region_xor"]:
+        size = case["size"]
+        a, b = shards(11, case["seed_stripe"], 2, size)
+        c = np.zeros(size + 16, np.uint8)
+        d["rxor"](a.ctypes.data, b.ctypes.data, c.ctypes.data, size)
+        run.check(fnv1a64(c[:size]) == case["digest"], f"region xor {size}")
+        d["rxor"](a.ctypes.data, b.ctypes.data, a.ctypes.data, size)  # r3 == r1
+        run.check(fnv1a64(a[:size]) == case["digest"], f"region xor r3 == r1 {size}")
+
+
+def surface(d, ref, ref_nsa, run):
+    rng = np.random.default_rng(5)
+    size = 64 << 10
+    for w, fn in ((16, "rmul16"), (32, "rmul32")):
+        r = ref_nsa if w == 16 else ref
+        for add in (0, 1):
+            src = rng.integers(0, 256, size + 16, dtype=np.uint8)
+            dst = rng.integers(0, 256, size + 16, dtype=np.uint8)
+            a, b = dst.copy(), dst.copy()
+            d[fn](src.ctypes.data, 0x1234 + w, size, a.ctypes.data, add)
+            r[fn](src.ctypes.data, 0x1234 + w, size, b.ctypes.data, add)
+            run.check(np.array_equal(a[:size], b[:size]), f"w{w} region multiply add={add}")
+        k, m = 6, 3
+        M = matrix(d, k, m, w)
+        data = [rng.integers(0, 256, size + 16, dtype=np.uint8) for _ in range(k)]
+        c1 = [np.zeros(size + 16, np.uint8) for _ in range(m)]
+        c2 = [np.zeros(size + 16, np.uint8) for _ in range(m)]
+        d["encode"](k, m, w, ints(M), ptrs(data), ptrs(c1), size)
+        r["encode"](k, m, w, ints(M), ptrs(data), ptrs(c2), size)
+        run.check(all(np.array_equal(a[:size], b[:size]) for a, b in zip(c1, c2)), f"w{w} matrix encode")
+    k, m, w, ps = 5, 2, 8, 1024
+    M = matrix(d, k, m)
+    bmp = d["to_bitmatrix"](k, m, w, ints(M))
+    BM = list((I * (k * m * w * w)).from_address(bmp))
+    bsize = w * ps * 3
+    data = [rng.integers(0, 256, bsize, dtype=np.uint8) for _ in range(k)]
+    c1 = [np.zeros(bsize, np.uint8) for _ in range(m)]
+    c2 = [np.zeros(bsize, np.uint8) for _ in range(m)]
+    d["bm_encode"](k, m, w, ints(BM), ptrs(data), ptrs(c1), bsize, ps)
+    ref["bm_encode"](k, m, w, ints(BM), ptrs(data), ptrs(c2), bsize, ps)
+    run.check(all(np.array_equal(a, b) for a, b in zip(c1, c2)), "bit-matrix encode")
+    sched = d["smart_sched"](k, m, w, ints(BM))
+    c3 = [np.zeros(bsize, np.uint8) for _ in range(m)]
+    d["sched_encode"](k, m, w, sched, ptrs(data), ptrs(c3), bsize, ps)
+    run.check(all(np.array_equal(a, b) for a, b in zip(c3, c2)), "schedule encode")
+    r6a = [np.zeros(size, np.uint8) for _ in range(2)]
+    r6b = [np.zeros(size, np.uint8) for _ in range(2)]
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(4)]
+    ra = d["r6"](4, 8, ptrs(data), ptrs(r6a), size)
+    rb = ref["r6"](4, 8, ptrs(data), ptrs(r6b), size)
+    run.check(ra == rb == 1 and all(np.array_equal(a, b) for a, b in zip(r6a, r6b)), "RAID-6 encode")
+    row = [1, 0, 71, 1, 200]
+    dst1 = rng.integers(0, 256, size, dtype=np.uint8)
+    dst2 = dst1.copy()
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(5)]
+    d["dotprod"](5, 8, ints(row), None, 5, ptrs(data), ptrs([dst1]), size)
+    ref["dotprod"](5, 8, ints(row), None, 5, ptrs(data), ptrs([dst2]), size)
+    run.check(np.array_equal(dst1, dst2), "dot product")
+    # aliasing: a coding buffer that is also a data buffer follows the
+    # reference's sequential semantics (jerasure.cpp:285-299)
+    k, m = 6, 3
+    M = matrix(d, k, m)
+
+    def aliased_encode(lib):
+        data = [np.array(x) for x in shards(41, 0, k, size, pad=0)]
+        coding = [data[3], np.zeros(size, np.uint8), np.zeros(size, np.uint8)]
+        lib["encode"](k, m, 8, ints(M), ptrs(data), ptrs(coding), size)
+        return np.concatenate(data + coding[1:]).tobytes()
+
+    run.check(aliased_encode(d) == aliased_encode(ref), "encode with coding[0] == data[3]")
+    src = rng.integers(0, 256, size, dtype=np.uint8)
+    a, b = src.copy(), src.copy()
+    d["rmul8"](a.ctypes.data, 77, size, None, 1)
+    ref["rmul8"](b.ctypes.data, 77, size, None, 1)
+    run.check(np.array_equal(a, b), "in-place region multiply")
+
+
+def main():
+    scenario = sys.argv[1]
+    with open(os.path.join(TESTS, "golden", "golden.json")) as fh:
+        golden = json.load(fh)
+    d = bind(os.path.join(LIB, "libjerasure_amd.so"))
+    run = Run(scenario)
+    if scenario == "client":
+        client(d, golden, run)
+    elif scenario == "ecx":
+        ecx(d, bind(os.path.join(REF, "libjerasure_ref.so")), golden, run)
+    elif scenario == "surface":
+        surface(d, bind(os.path.join(REF, "libjerasure_ref.so")), bind(os.path.join(REF, "libjerasure_ref_nsa.so")),
+                run)
+    else:
+        raise SystemExit(f"unknown scenario {scenario}")
+    core = ctypes.CDLL(os.path.join(LIB, "libecgpu.so"))
+    core.ecgpu_fallback_count.restype = ctypes.c_int64
+    core.ecgpu_device_lost.restype = ctypes.c_int
+    print(json.dumps({"scenario": scenario, "checked": run.checked, "mismatches": run.mismatches[:20],
+                      "fallbacks": int(core.ecgpu_fallback_count()), "lost": int(core.ecgpu_device_lost(0))}),
+          flush=True)
+    return 0 if not run.mismatches else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,8 +1,10 @@
 // host_harness.cpp -- drives the HOST-ONLY part of libecgpu (field tables,
 // matrix construction / inversion, the decode planner, bit-matrix and
-// schedule construction, the buffer contract, knobs; csrc/{gf_host,
-// matrix_host,planner,schedule_host,capi_host,contract_host,knobs}.cpp) under AddressSanitizer + UBSan, or ThreadSanitizer with
-// `threads` > 1 (first-use table initialisation races between callers).
+// schedule construction, the buffer contract, knobs, the CPU fallback's
+// executor and bookkeeping; csrc/{gf_host,matrix_host,planner,schedule_host,
+// capi_host,contract_host,knobs,cpu_fallback}.cpp) under AddressSanitizer +
+// UBSan, or ThreadSanitizer with `threads` > 1 (first-use table
+// initialisation races between callers).
 // Built and run by tests/test_sanitizers.py.  No GPU code is linked: the one
 // device entry point the host objects reference is stubbed and never called.
 //
@@ -14,7 +16,10 @@
 #include <thread>
 #include <vector>
 
+#include "cpu_fallback.hpp"
 #include "ecgpu.h"
+#include "gf_host.hpp"
+#include "planner.hpp"
 
 extern "C" int ecgpu_schedule_run(int, char**, int**, int, int, int) {
   std::fprintf(stderr, "ecgpu_schedule_run: GPU entry point called from the host harness\n");
@@ -163,8 +168,113 @@ void knobs_and_split_tables() {
            "split multiply", x);
 }
 
+// The CPU fallback's executor (cpu_fallback.cpp) against the reference's
+// SEQUENTIAL semantics: random sequences of whole-region copy / XOR /
+// multiply(-add) over a few buffers -- aliasing included (a destination that
+// is also a source, r3 == r1) -- run op by op on one copy of the buffers, and
+// planned into one fused map (LinearTracker) run by cpu_apply on another.
+// Sizes straddle the executor's 64 KiB chunks and are whole w-bit words.
+// Then the packet form (PacketTracker + cpu_apply_packets) the same way.
+uint32_t word_at(const std::vector<uint8_t>& b, size_t i, int w) {
+  uint32_t v = 0;
+  std::memcpy(&v, b.data() + i * size_t(w / 8), size_t(w / 8));
+  return v;
+}
+
+void set_word(std::vector<uint8_t>& b, size_t i, int w, uint32_t v) { std::memcpy(b.data() + i * size_t(w / 8), &v, size_t(w / 8)); }
+
+void cpu_fallback_exec(unsigned seed) {
+  using ecgpu::FusedOp;
+  using ecgpu::LinearTracker;
+  auto rnd = [&]() {
+    seed = seed * 1103515245u + 12345u;
+    return seed >> 8;
+  };
+  for (int trial = 0; trial < 24; ++trial) {
+    const int w = trial % 3 == 0 ? 8 : trial % 3 == 1 ? 16 : 32;
+    const int nbuf = 2 + int(rnd() % 4);
+    const size_t n = size_t(w / 8) * (1 + rnd() % ((70u << 10) / unsigned(w / 8)));
+    const uint32_t mask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
+    std::vector<std::vector<uint8_t>> seq(static_cast<size_t>(nbuf)), fused;
+    for (auto& b : seq) {
+      b.resize(n);
+      for (auto& x : b) x = uint8_t(rnd());
+    }
+    fused = seq;
+    LinearTracker t(w);
+    std::vector<void*> id(static_cast<size_t>(nbuf));
+    for (int i = 0; i < nbuf; ++i) id[size_t(i)] = fused[size_t(i)].data();
+    const int nops = 1 + int(rnd() % 6);
+    for (int o = 0; o < nops; ++o) {
+      const int a = int(rnd() % unsigned(nbuf)), b = int(rnd() % unsigned(nbuf)), c = int(rnd() % unsigned(nbuf));
+      const int kind = int(rnd() % 3);
+      const size_t words = n / size_t(w / 8);
+      if (kind == 0) {  // b = a
+        seq[size_t(b)] = std::vector<uint8_t>(seq[size_t(a)]);
+        t.copy(id[size_t(b)], id[size_t(a)]);
+      } else if (kind == 1) {  // c = a ^ b
+        std::vector<uint8_t> r(n);
+        for (size_t i = 0; i < n; ++i) r[i] = seq[size_t(a)][i] ^ seq[size_t(b)][i];
+        seq[size_t(c)] = r;
+        t.xor3(id[size_t(a)], id[size_t(b)], id[size_t(c)]);
+      } else {  // b (^)= k * a
+        const uint32_t k = uint32_t(rnd()) & mask;
+        const bool add = rnd() & 1;
+        std::vector<uint8_t> r = seq[size_t(b)];
+        for (size_t i = 0; i < words; ++i) {
+          const uint32_t p = ecgpu::gf_mul_poly(word_at(seq[size_t(a)], i, w), k, w);
+          set_word(r, i, w, add ? (word_at(r, i, w) ^ p) : p);
+        }
+        seq[size_t(b)] = r;
+        t.mul(id[size_t(a)], int(k), id[size_t(b)], add);
+      }
+    }
+    ecgpu::rt::cpu_apply(t.finish(), int64_t(n));
+    for (int i = 0; i < nbuf; ++i) expect(fused[size_t(i)] == seq[size_t(i)], "cpu_apply vs sequential", trial, i);
+  }
+  // packets: slots x rows of ps bytes, super-packets nsp apart
+  for (int trial = 0; trial < 12; ++trial) {
+    const int nslots = 2 + int(rnd() % 3), nrows = 1 + int(rnd() % 4), nsp = 1 + int(rnd() % 3);
+    const int64_t ps = 8 * (1 + int64_t(rnd() % 64)), spstride = ps * nrows;
+    std::vector<std::vector<char>> seq(size_t(nslots), std::vector<char>(size_t(spstride * nsp)));
+    for (auto& b : seq)
+      for (auto& x : b) x = char(rnd());
+    auto fused = seq;
+    ecgpu::PacketTracker t(nslots, nrows);
+    const int nops = 1 + int(rnd() % 8);
+    for (int o = 0; o < nops; ++o) {
+      const int ss = int(rnd() % unsigned(nslots)), sr = int(rnd() % unsigned(nrows));
+      const int ds = int(rnd() % unsigned(nslots)), dr = int(rnd() % unsigned(nrows));
+      const bool x = rnd() & 1;
+      for (int sp = 0; sp < nsp; ++sp)
+        for (int64_t i = 0; i < ps; ++i) {
+          char& d = seq[size_t(ds)][size_t(sp * spstride + dr * ps + i)];
+          const char s = seq[size_t(ss)][size_t(sp * spstride + sr * ps + i)];
+          d = x ? char(d ^ s) : s;
+        }
+      if (x) t.xor_into(ds, dr, ss, sr);
+      else t.copy(ds, dr, ss, sr);
+    }
+    std::vector<char*> ptrs;
+    for (auto& b : fused) ptrs.push_back(b.data());
+    ecgpu::rt::cpu_apply_packets(t.finish(), ptrs, nsp, spstride, ps);
+    for (int i = 0; i < nslots; ++i) expect(fused[size_t(i)] == seq[size_t(i)], "cpu_apply_packets", trial, i);
+  }
+  // the bookkeeping, concurrently under TSan
+  const int64_t before = ecgpu_fallback_count();
+  ecgpu::rt::record_fallback("harness", "test");
+  expect(ecgpu_fallback_count() >= before + 1, "fallback count");
+  ecgpu::rt::trace_begin();
+  expect(!ecgpu::rt::caller_written(), "trace begin");
+  ecgpu::rt::note_caller_write();
+  expect(ecgpu::rt::caller_written(), "caller write noted");
+  ecgpu::rt::mark_device_lost(5);
+  expect(ecgpu_device_lost(5) == 1 && ecgpu_device_lost(4) == 0, "device lost bits");
+}
+
 void run_all() {
   knobs_and_split_tables();
+  cpu_fallback_exec(0xFA11u);
   known_answers();
   matrices();
   decode_plans();

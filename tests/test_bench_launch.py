@@ -161,3 +161,50 @@ def test_cpu_baseline_thread_split_keeps_parity(threads):
     for _ in range(3):
         base, ok = bench.cpu_baseline(0.2, stripe, k, m, [0], threads=threads, cpus=cpus)
         assert ok and base["cores"] == threads
+
+
+# ---------------------------------------------- N > 1 e2e ----
+def test_parse_cpulist_and_node_lookup(tmp_path):
+    import bench
+    assert bench.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert bench.parse_cpulist("") == set()
+    pci = tmp_path / "pci" / "0000:8e:00.0"
+    pci.mkdir(parents=True)
+    (pci / "numa_node").write_text("1\n")
+    assert bench.pci_numa_node("0000:8E:00.0", sysfs=str(tmp_path / "pci")) == 1
+    (pci / "numa_node").write_text("-1\n")  # no affinity reported
+    assert bench.pci_numa_node("0000:8e:00.0", sysfs=str(tmp_path / "pci")) is None
+    assert bench.pci_numa_node(None) is None and bench.pci_numa_node("0000:ff:00.0", sysfs=str(tmp_path)) is None
+    node = tmp_path / "node" / "node1"
+    node.mkdir(parents=True)
+    (node / "cpulist").write_text("48-95,144-191\n")
+    assert bench.node_cpus(1, sysfs=str(tmp_path / "node")) == set(range(48, 96)) | set(range(144, 192))
+    assert bench.node_cpus(7, sysfs=str(tmp_path / "node")) == set()
+
+
+def test_page_numa_node_of_own_memory():
+    import numpy as np
+
+    import bench
+    a = np.ones(1 << 20, np.uint8)
+    n = bench.page_numa_node(a.ctypes.data)
+    assert n is None or n >= 0
+
+
+def test_e2e_aggregate_is_total_over_slowest():
+    import bench
+    rank = lambda ms_e, ms_d, ok=True: {"data_bytes_per_pass": 10 * 2**30,  # noqa: E731
+                                        "encode": {"pass_ms": ms_e, "data_GiBps": 10 / (ms_e / 1e3),
+                                                   "parity_ok": ok},
+                                        "decode": {"pass_ms": ms_d, "data_GiBps": 10 / (ms_d / 1e3),
+                                                   "rebuilt_ok": True}}
+    agg = bench.e2e_aggregate([rank(200.0, 250.0), rank(250.0, 200.0), rank(100.0, 100.0)])
+    assert agg["ranks"] == 3
+    assert agg["encode"]["data_GiBps"] == round(30 / 0.25, 2) and agg["encode"]["slowest_pass_ms"] == 250.0
+    assert agg["decode"]["data_GiBps"] == round(30 / 0.25, 2) and agg["encode"]["ok"] and agg["decode"]["ok"]
+    assert agg["encode"]["per_rank_GiBps"] == [50.0, 40.0, 100.0]
+    bad = bench.e2e_aggregate([rank(1.0, 1.0), rank(1.0, 1.0, ok=False)])
+    assert bad["encode"]["ok"] is False
+    enc_only = bench.e2e_aggregate([{"data_bytes_per_pass": 2**30, "encode": {"pass_ms": 10.0, "data_GiBps": 100.0,
+                                                                            "parity_ok": True}}])
+    assert "decode" not in enc_only and enc_only["encode"]["data_GiBps"] == 100.0

@@ -31,7 +31,63 @@ def test_library_is_built_from_these_sources():
     ids = b.build_ids()
     assert lib.ecgpu_build_id(0).decode() == ids["build"], "libecgpu.so is stale: rebuild"
     assert lib.ecgpu_build_id(1).decode() == ids["kernels"]
-    assert len(ids["build"]) == 16 and ids["build"] != ids["kernels"]
+    assert lib.ecgpu_build_id(2).decode() == ids["wide"]
+    assert lib.ecgpu_build_id(3).decode() == ids["packets"]
+    assert len(ids["build"]) == 16 and len({ids["build"], ids["kernels"], ids["wide"], ids["packets"]}) == 4
+
+
+def _ids_with_edit(b, tmp_path, name, text=None):
+    """build_ids() over a copy of csrc/ with one file appended to (or a knob
+    row's default changed: text = (old, new))."""
+    import shutil
+    csrc = tmp_path / "csrc"
+    if csrc.exists():
+        shutil.rmtree(csrc)
+    shutil.copytree(b.CSRC, csrc)
+    f = csrc / name
+    if isinstance(text, tuple):
+        f.write_text(f.read_text().replace(*text))
+    else:
+        f.write_text(f.read_text() + "\n// edited\n")
+    saved = b.CSRC
+    b.CSRC = str(csrc)
+    try:
+        return b.build_ids()
+    finally:
+        b.CSRC = saved
+
+
+def test_kernel_families_have_their_own_build_ids(tmp_path):
+    """an edit to a w = 32, packet or lab kernel must not
+    invalidate the w = 8 PMC records (keyed to ecgpu_build_id(1))."""
+    b = _build_module()
+    base = b.build_ids()
+    for name in ("gf_kernels_wide.hpp", "gf_kernels_packets.hpp", "dispatch_wide.hip", "wide_spec.hip",
+                 "packets.hip", "diag_kernels_w8.hpp", "diag_kernels.hip", "ecgpu_runtime.hip", "cpu_fallback.cpp"):
+        ids = _ids_with_edit(b, tmp_path, name)
+        assert ids["kernels"] == base["kernels"], name
+        assert ids["build"] != base["build"] or name.startswith("diag_kernels"), name
+    for name in ("gf_kernels_w8.hpp", "gf_spec.hip", "dispatch_w8.hip"):
+        assert _ids_with_edit(b, tmp_path, name)["kernels"] != base["kernels"], name
+    assert _ids_with_edit(b, tmp_path, "gf_kernels_wide.hpp")["wide"] != base["wide"]
+    assert _ids_with_edit(b, tmp_path, "gf_kernels_packets.hpp")["packets"] != base["packets"]
+    # the defaults of the knobs a family's dispatch reads are part of its ID, others are not
+    cap = _ids_with_edit(b, tmp_path, "knobs.cpp", ('{"ECGPU_CAP", "cap", -1}', '{"ECGPU_CAP", "cap", 1}'))
+    assert cap["kernels"] != base["kernels"] and cap["wide"] == base["wide"]
+    pipe = _ids_with_edit(b, tmp_path, "knobs.cpp", ('{"ECGPU_WIDE_PIPE", "wide_pipe", 1}',
+                                                     '{"ECGPU_WIDE_PIPE", "wide_pipe", 2}'))
+    assert pipe["kernels"] == base["kernels"] and pipe["wide"] != base["wide"]
+
+
+def test_lab_kernels_are_not_in_the_production_library():
+    import shutil
+    import subprocess
+    if not shutil.which("nm"):
+        pytest.skip("nm not installed")
+    out = subprocess.run(["nm", "-C", LIB], capture_output=True, text=True, check=True).stdout
+    for k in ("gf_apply_dma", "gf_apply_occ8", "gf_apply_perm_stream", "gf_apply_perm<", "diag_copy"):
+        assert k not in out, k
+    assert "gf_apply<10, 4, 3" in out
 
 
 def test_rebuild_decision_is_content_based(tmp_path):

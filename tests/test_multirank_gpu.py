@@ -172,11 +172,21 @@ def test_bench_gpus2_rehearsal_spawns_two_ranks(gpu):
                 "C4_decode_0123", "C5_encode"} <= set(p["configs"])
         assert p["configs"]["C4_decode_0123"]["frac"] > 0
     assert d["configs"]["C3_decode_parity"]["algorithmic_bytes_per_launch"] == 11 * (4 << 20) * 4
-    # rank 0's PCIe-inclusive host-pipeline rates, after every rank's timed work
+    # PCIe-inclusive host-pipeline rates: every rank runs
+    # its own pass at once after the timed work; the line carries each rank's
+    # rates (and where its pinned buffers live) and the whole job's
     e2e = d["e2e"]
     assert e2e["encode"]["parity_ok"] and e2e["encode"]["data_GiBps"] > 1
     assert e2e["decode"]["rebuilt_ok"] and e2e["decode"]["erasures"] == [0]
     assert d["e2e_ok"] is True
+    assert len(d["e2e_per_rank"]) == 2 and d["e2e_per_rank"][0] == e2e
+    for r_ in d["e2e_per_rank"]:
+        assert r_["encode"]["parity_ok"] and r_["decode"]["rebuilt_ok"] and "host_numa_node" in r_
+        assert "gpu_numa_node" in r_ and "threads_on_gpu_node" in r_
+    agg = d["e2e_aggregate"]
+    assert agg["ranks"] == 2 and agg["encode"]["ok"] and agg["decode"]["ok"]
+    assert agg["encode"]["data_GiBps"] > 0 and len(agg["encode"]["per_rank_GiBps"]) == 2
+    assert d["cpu_fallbacks"] == 0 and all(p["cpu_fallbacks"] == 0 for p in d["per_rank"])
     # each rank names its physical GPU; both sit on cuda:0 here, which the
     # rehearsal flag exempts from the distinct-device check
     buses = [p["pci_bus_id"] for p in d["per_rank"]]

@@ -41,6 +41,7 @@ VARIANTS = {
     "default": {},
     "cap_never": {"cap": 0},
     "cap_always": {"cap": 1},
+    "bpcu6_always": {"cap": 1, "blocks_per_cu": 6},
     "bpcu5_always": {"cap": 1, "blocks_per_cu": 5},
     "bpcu4_always": {"cap": 1, "blocks_per_cu": 4},
     "bpcu3_always": {"cap": 1, "blocks_per_cu": 3},

@@ -21,10 +21,11 @@ int fail(int code, const std::string& msg);  // capi_host.cpp
 
 namespace {
 
-// Bytes of every buffer processed per step: all sources of the step are read
+// Bytes of every buffer processed per step (32 KiB: 14 RS(10,4) buffers stay in
+// a core's L2): all sources of the step are read
 // into the outputs' temporaries before any output is written, the kernel's
 // per-column order.  A multiple of 4 (whole w = 16 / 32 words).
-constexpr int64_t kChunk = int64_t(64) << 10;
+constexpr int64_t kChunk = int64_t(32) << 10;
 
 // ---- GF(2^8): c*x = lo[x & 15] ^ hi[x >> 4] (the north star's nibble split)
 struct Nib8 {
@@ -97,8 +98,31 @@ void mul_addw(uint8_t* acc, const uint8_t* src, int64_t n, const NibW<Word>& t) 
   }
 }
 
+void xor_into_scalar(uint8_t* acc, const uint8_t* src, int64_t n) {
+  int64_t i = 0;
+  for (; i + 8 <= n; i += 8) {  // 8-byte words (the library builds at -O2, which does not vectorise)
+    uint64_t a, b;
+    std::memcpy(&a, acc + i, 8);
+    std::memcpy(&b, src + i, 8);
+    a ^= b;
+    std::memcpy(acc + i, &a, 8);
+  }
+  for (; i < n; ++i) acc[i] ^= src[i];
+}
+
+__attribute__((target("avx2"))) void xor_into_avx2(uint8_t* acc, const uint8_t* src, int64_t n) {
+  int64_t i = 0;
+  for (; i + 32 <= n; i += 32) {
+    const __m256i x = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(acc + i));
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(acc + i), _mm256_xor_si256(a, x));
+  }
+  xor_into_scalar(acc + i, src + i, n - i);
+}
+
 void xor_into(uint8_t* acc, const uint8_t* src, int64_t n) {
-  for (int64_t i = 0; i < n; ++i) acc[i] ^= src[i];
+  if (have_avx2()) xor_into_avx2(acc, src, n);
+  else xor_into_scalar(acc, src, n);
 }
 
 // Per-term table of one call (coefficients 0 and 1 need none).

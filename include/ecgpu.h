@@ -315,10 +315,11 @@ ECGPU_API int ecgpu_host_unregister(void* ptr);
 
 /* HBM layout advice for callers that allocate their own shard slabs:
  * the byte distance to put between consecutive shards (and stripes) of
- * `size`-byte shards.  Shards at power-of-two strides send a column's k+m
- * accesses to the same HBM channel / bank on different rows; skewing every
- * shard by 10 KiB spreads them at every shard size measured (64 KiB-16 MiB;
- * +41 % over no skew on RS(10,4) 4 MiB). */
+ * `size`-byte shards: round_up(size, 256) plus a skew.  Shards at
+ * power-of-two strides send a column's k+m accesses to the same HBM channel /
+ * bank on different rows; the skew comes from a per-size table measured on
+ * MI355X (6 KiB at 4 MiB, 8 KiB at 16 MiB, none at 1 MiB; 10 KiB for sizes
+ * not in the table; shard_stride.hpp). */
 ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size);
 
 /* Convenience: encode `stripes` device-resident stripes with the m x k

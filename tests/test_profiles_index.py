@@ -20,3 +20,38 @@ def test_bench_traffic_record_is_committed():
     assert summary["kernel_build_id"] and summary["kernels"]["encode"]["traffic_over_algorithmic"] < 1.01
     for f in ("pmc_encode.json", "pmc_decode.json", "r04_kernel_stats.csv", "r04_bench.json"):
         assert os.path.exists(os.path.join(PROF, f)), f
+
+
+def _skew_table():
+    """{size: skew} from csrc/shard_stride.hpp's kSkewTable."""
+    import re
+    src = open(os.path.join(ROOT, "erasure_coding_test_amd", "csrc", "shard_stride.hpp")).read()
+    body = src[src.index("kSkewTable[] = {"):src.index("};", src.index("kSkewTable[] = {"))]
+    def ev(e):  # "12 << 10" -> 12288
+        parts = [int(x) for x in e.split("<<")]
+        return parts[0] << sum(parts[1:])
+    return {ev(a): ev(b) for a, b in re.findall(r"\{([\d <]+),\s*([\d <]+)\}", body)}
+
+
+def test_stride_statements_agree_with_the_table():
+    """the bench's stride comment, the C header and the
+    DESIGN §4 table state the skews the library actually uses."""
+    import re
+    t = _skew_table()
+    mib, kib = 1 << 20, 1 << 10
+    assert t[4 * mib] == 6 * kib and t[16 * mib] == 8 * kib and t[1 * mib] == 0
+    bench_src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "6 KiB at 4 MiB, 8 KiB at 16 MiB" in bench_src and "S + 10 KiB" not in bench_src
+    hdr = open(os.path.join(ROOT, "include", "ecgpu.h")).read()
+    assert "6 KiB at 4 MiB, 8 KiB at 16 MiB, none at 1 MiB" in hdr
+    design = open(os.path.join(ROOT, "DESIGN.md")).read()
+    sizes = re.search(r"\| shard size \(±1/16\) \|(.*)\|", design).group(1).split("|")
+    skews = re.search(r"\| skew \(KiB\) \|(.*)\|", design).group(1).split("|")
+    got = {}
+    for sz, sk in zip(sizes, skews):
+        sz, sk = sz.strip(), sk.strip().strip("*")
+        if sz == "other":
+            continue
+        n = int(sz.split()[0]) * (kib if sz.endswith("K") else mib)
+        got[n] = int(sk) * kib
+    assert got == t

@@ -79,6 +79,9 @@ def main():
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--tag", default="")
+    ap.add_argument("--probes", action="store_true",
+                    help="after each shape's launches, its XOR stream probe (bench.xor_stream_probe) on the same slab: "
+                         "per-dispatch PMC of kernel and probe side by side (effective clock, round 5)")
     a = ap.parse_args()
     shapes = a.shapes.split(",")
     variants = ["default"] if a.pmc else a.variants.split(",")
@@ -98,6 +101,10 @@ def main():
                 ms = bench.time_launches(lambda: p.launch(stream.cuda_stream), stream, a.reps, warmup=2)
                 times[(s, v)].append(ms)
                 p.close()
+                if a.probes:
+                    k, m, S, B, er = SHAPES[s]
+                    slab = slabs[(k, m, S, B)][0]
+                    bench.xor_stream_probe(slab, S, k, m if er is None else len(er), reps=a.reps)
         N.reset_knob(None)
     for s in shapes:
         base = statistics.median(times[(s, "default")])

@@ -1,7 +1,9 @@
 """Inline (gf_apply_inl, tables in the kernel arguments) vs plan launch
 (gf_apply, tables in HBM) for one-stripe device-resident calls whose launch
 is dense in multiplies: RS(k,4) random-matrix encode, 64 MiB shards.
-Run under rocprofv3 --kernel-trace --stats; ECGPU_INLINE is read per call.
+Run under rocprofv3 --kernel-trace --stats.  The knob ECGPU_INLINE is read
+once per process (knobs.hpp), so the two arms are switched in-process with
+ecgpu_set_knob between calls and restored at the end.
 
     rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/inl -o run -- python3 tools/probe_inline.py
 """
@@ -39,6 +41,7 @@ def main():
                     ref = out
                 assert torch.equal(out, ref), (k, inl)
         print(f"k={k}: inline and plan outputs equal")
+    N.reset_knob("ECGPU_INLINE")
 
 
 if __name__ == "__main__":

@@ -153,3 +153,31 @@ def test_device_buffers_never_fall_back_gpu(gpu, knobs):
     knobs.reset("ECGPU_TEST_INJECT_HIP")
     J.jerasure_matrix_encode(k, m, 8, M, d, c, size)  # row 0 of the Vandermonde matrix is all ones
     assert np.array_equal(c[0].cpu().numpy(), np.full(size, 1 ^ 2 ^ 3 ^ 4, np.uint8))
+
+
+def fuzz(cases, inject, seed=20261017):
+    env = dict(os.environ, ECGPU_CPU_FALLBACK="1", ECGPU_TEST_INJECT_HIP=str(inject))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "fallback_fuzz.py"), str(cases), str(seed)],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]) if r.stdout.strip() else None
+    return r, out
+
+
+def test_fallback_fuzz_vs_reference():
+    """3,000 random synchronous calls (a quarter with repeated buffers) completed
+    on the CPU fallback, bytes and return codes equal to the compiled reference."""
+    _need_reference()
+    r, out = fuzz(3000, inject=2)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert out["mismatches"] == [] and out["fallbacks"] >= 2500, out
+    assert all(v > 0 for v in out["kinds"].values()), out
+
+
+@pytest.mark.gpu
+def test_fallback_fuzz_vs_reference_gpu():
+    """The same on the MI355X, each call's GPU attempt failing before its first
+    launch (transient injection): the fallback decision after map_buffers."""
+    _need_reference()
+    r, out = fuzz(1000, inject=1, seed=77)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert out["mismatches"] == [] and out["fallbacks"] >= 800, out

@@ -1,8 +1,11 @@
 // schedule_host.cpp -- see schedule_host.hpp.
 #include "schedule_host.hpp"
 
+#include <cstddef>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "matrix_host.hpp"
 
@@ -41,64 +44,64 @@ int** dumb_bitmatrix_to_schedule(int k, int m, int w, const int* bitmatrix) {
   return ops;
 }
 
-// Greedy reuse: repeatedly emit the pending row that is cheapest to build,
-// either from scratch (popcount) or as a copy of an already-built row plus
-// the XOR of the differing bits (1 + Hamming distance).
+// Greedy reuse (jerasure.cpp:1226-1344, the op list is caller-visible so the
+// choices must be the reference's): each output row is built either from
+// scratch (a copy then XORs: popcount ops) or as a copy of an already-built
+// output row plus the XOR of the bits where the two differ (1 + Hamming
+// distance).  Rows are held as 64-bit bitsets, so a distance is a few
+// popcounts; each step takes the FIRST pending row (in row order) of least
+// cost, then lowers the costs of the rows still pending against the row
+// just built.
 int** smart_bitmatrix_to_schedule(int k, int m, int w, const int* bitmatrix) {
-  const int rows = m * w, cols = k * w;
-  int** ops = static_cast<int**>(std::malloc(sizeof(int*) * (size_t(k) * m * w * w + 1)));
-  int n = 0;
-  std::vector<int> cost(static_cast<size_t>(rows)), from(static_cast<size_t>(rows), -1),
-      next(static_cast<size_t>(rows)), prev(static_cast<size_t>(rows));
-  int best = 0, best_cost = cols + 1;
+  const int rows = m * w, cols = k * w, words = (cols + 63) / 64;
+  std::vector<uint64_t> set(size_t(rows) * size_t(words), 0);
+  for (int r = 0; r < rows; ++r)
+    for (int c = 0; c < cols; ++c)
+      if (bitmatrix[r * cols + c]) set[size_t(r) * words + size_t(c / 64)] |= uint64_t(1) << (c % 64);
+  auto row_bits = [&](int r) { return set.data() + size_t(r) * size_t(words); };
+  auto distance = [&](int a, int b) {
+    int d = 0;
+    for (int i = 0; i < words; ++i) d += __builtin_popcountll(row_bits(a)[i] ^ row_bits(b)[i]);
+    return d;
+  };
+  std::vector<int> cost(static_cast<size_t>(rows)), base(static_cast<size_t>(rows), -1), pending;
   for (int r = 0; r < rows; ++r) {
     int pop = 0;
-    for (int c = 0; c < cols; ++c) pop += bitmatrix[r * cols + c];
-    cost[r] = pop;
-    next[r] = r + 1;
-    prev[r] = r - 1;
-    if (pop < best_cost) {
-      best_cost = pop;
-      best = r;
-    }
+    for (int i = 0; i < words; ++i) pop += __builtin_popcountll(row_bits(r)[i]);
+    cost[size_t(r)] = pop;
+    pending.push_back(r);
   }
-  next[rows - 1] = -1;
-  int head = 0;
-  while (head != -1) {
-    const int row = best;
-    if (prev[row] == -1) {  // unlink row from the pending list
-      head = next[row];
-      if (head != -1) prev[head] = -1;
-    } else {
-      next[prev[row]] = next[row];
-      if (next[row] != -1) prev[next[row]] = prev[row];
-    }
-    const int* bits = bitmatrix + row * cols;
-    if (from[row] == -1) {
-      int xor_flag = 0;
-      for (int c = 0; c < cols; ++c)
-        if (bits[c]) {
-          ops[n++] = make_op(c / w, c % w, k + row / w, row % w, xor_flag);
-          xor_flag = 1;
-        }
-    } else {
-      ops[n++] = make_op(k + from[row] / w, from[row] % w, k + row / w, row % w, 0);
-      const int* base = bitmatrix + from[row] * cols;
-      for (int c = 0; c < cols; ++c)
-        if (bits[c] ^ base[c]) ops[n++] = make_op(c / w, c % w, k + row / w, row % w, 1);
-    }
-    best_cost = cols + 1;
-    for (int r = head; r != -1; r = next[r]) {
-      int d = 1;
-      const int* other = bitmatrix + r * cols;
-      for (int c = 0; c < cols; ++c) d += bits[c] ^ other[c];
-      if (d < cost[r]) {
-        from[r] = row;
-        cost[r] = d;
+  int** ops = static_cast<int**>(std::malloc(sizeof(int*) * (size_t(k) * m * w * w + 1)));
+  int n = 0;
+  // the ops that build output row `row` from the sources where `bits` is set
+  auto emit_bits = [&](int row, const uint64_t* bits, int first_xor) {
+    int xor_flag = first_xor;
+    for (int c = 0; c < cols; ++c)
+      if (bits[c / 64] >> (c % 64) & 1u) {
+        ops[n++] = make_op(c / w, c % w, k + row / w, row % w, xor_flag);
+        xor_flag = 1;
       }
-      if (cost[r] < best_cost) {
-        best_cost = cost[r];
-        best = r;
+  };
+  std::vector<uint64_t> diff(static_cast<size_t>(words));
+  while (!pending.empty()) {
+    size_t at = 0;
+    for (size_t i = 1; i < pending.size(); ++i)
+      if (cost[size_t(pending[i])] < cost[size_t(pending[at])]) at = i;
+    const int row = pending[at];
+    pending.erase(pending.begin() + std::ptrdiff_t(at));
+    const int from = base[size_t(row)];
+    if (from < 0) {
+      emit_bits(row, row_bits(row), 0);
+    } else {
+      ops[n++] = make_op(k + from / w, from % w, k + row / w, row % w, 0);
+      for (int i = 0; i < words; ++i) diff[size_t(i)] = row_bits(row)[i] ^ row_bits(from)[i];
+      emit_bits(row, diff.data(), 1);
+    }
+    for (int r : pending) {
+      const int d = 1 + distance(row, r);
+      if (d < cost[size_t(r)]) {
+        cost[size_t(r)] = d;
+        base[size_t(r)] = row;
       }
     }
   }

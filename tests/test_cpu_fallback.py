@@ -34,10 +34,11 @@ DRIVER = os.path.join(ROOT, "tests", "fallback_driver.py")
 SCENARIOS = ["client", "ecx", "surface"]
 
 
-def drive(scenario, fallback, inject, timeout=600):
+def drive(scenario, fallback, inject, timeout=600, extra_env=None):
     env = dict(os.environ)
     env["ECGPU_CPU_FALLBACK"] = str(fallback)
     env["ECGPU_TEST_INJECT_HIP"] = str(inject)
+    env.update(extra_env or {})
     r = subprocess.run([sys.executable, DRIVER, scenario], capture_output=True, text=True, timeout=timeout, env=env,
                        cwd=ROOT)
     out = None
@@ -106,6 +107,17 @@ def test_fallback_after_injected_hip_error_gpu(scenario):
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
     assert out["mismatches"] == [] and out["checked"] > 0, out
     assert out["fallbacks"] >= 1 and out["lost"] == 0, out
+
+
+@pytest.mark.gpu
+def test_split_call_ranges_fall_back_independently_gpu():
+    """A call cut into concurrent byte ranges (ECGPU_SPLIT): each range's GPU
+    attempt fails and that range completes on the CPU on its own thread; the
+    call's bytes are the whole call's."""
+    _need_reference()
+    r, out = drive("client", fallback=1, inject=1, extra_env={"ECGPU_SPLIT": "3", "ECGPU_SPLIT_MIN_KIB": "256"})
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert out["mismatches"] == [] and out["fallbacks"] >= 1 and out["lost"] == 0, out
 
 
 @pytest.mark.gpu

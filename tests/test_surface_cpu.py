@@ -486,3 +486,26 @@ def test_python_schedule_construction_matches_reference(libs, k, m, w):
     assert bm == list(np.ctypeslib.as_array(ctypes.cast(bm_ref, IP), shape=(k * m * w * w,)))
     assert E.jerasure.jerasure_dumb_bitmatrix_to_schedule(k, m, w, bm) == read_schedule(ref.dumb(k, m, w, bm_ref))
     assert E.jerasure.jerasure_smart_bitmatrix_to_schedule(k, m, w, bm) == read_schedule(ref.smart(k, m, w, bm_ref))
+
+
+def test_schedules_of_random_bitmatrices_match_reference(libs):
+    """Both schedule builders on random (not only Vandermonde) bit-matrices,
+    including all-zero and repeated rows (ties in the smart builder's greedy
+    choice): the op lists equal the reference's exactly
+    (jerasure.cpp:1194-1224, :1226-1344)."""
+    ref, mine = libs
+    rnd = random.Random(1226)
+    for trial in range(60):
+        k, m, w = rnd.randint(1, 6), rnd.randint(1, 4), rnd.choice([1, 2, 3, 4, 8])
+        rows, cols = m * w, k * w
+        dens = rnd.choice([0.1, 0.3, 0.5, 0.8])
+        bm = [1 if rnd.random() < dens else 0 for _ in range(rows * cols)]
+        if rows > 1 and trial % 3 == 0:  # a repeated row and an all-zero row
+            r0, r1 = rnd.randrange(rows), rnd.randrange(rows)
+            bm[r1 * cols:(r1 + 1) * cols] = bm[r0 * cols:(r0 + 1) * cols]
+            z = rnd.randrange(rows)
+            bm[z * cols:(z + 1) * cols] = [0] * cols
+        for name in ("dumb", "smart"):
+            a = read_schedule(getattr(ref, name)(k, m, w, ints(bm)))
+            b = read_schedule(getattr(mine, name)(k, m, w, ints(bm)))
+            assert a == b, (trial, name, k, m, w)

@@ -837,12 +837,22 @@ def selftest_main(args):
     # a stand-in device identity per rank (ECGPU_SELFTEST_SAME_BUS=1: every
     # rank claims one device, which the distinct-device check must fail)
     bus = "selftest:00" if os.environ.get("ECGPU_SELFTEST_SAME_BUS") == "1" else f"selftest:{local:02d}"
-    per_rank = gather({"rank": rank, "local_rank": local, "world": world, "pid": os.getpid(), "pci_bus_id": bus},
-                      world)
+    # a stand-in e2e pass per rank, through the same barrier-started timing,
+    # gather and aggregation as the real N > 1 e2e leg (e2e_all_ranks)
+    barrier(world)
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    pass_ms = (time.perf_counter() - t0) * 1e3
+    e2e = {"data_bytes_per_pass": 1 << 30, "host_numa_node": None, "gpu_numa_node": pci_numa_node(None),
+           "encode": {"pass_ms": round(pass_ms, 2), "data_GiBps": round(1e3 / pass_ms, 2), "parity_ok": True}}
+    per_rank = gather({"rank": rank, "local_rank": local, "world": world, "pid": os.getpid(), "pci_bus_id": bus,
+                       "e2e": e2e}, world)
     devices_ok, devices_note = distinct_devices(per_rank, os.environ.get("ECGPU_BENCH_ONE_DEVICE") == "1")
     if rank == 0:
+        e2e_per_rank = [p.pop("e2e") for p in per_rank]
         print(json.dumps({"selftest": True, "n_gpus": world, "max_over_ranks": t, "per_rank": per_rank,
                           "stripes": {r: global_stripe_ids(2, r, world) for r in range(world)},
+                          "e2e_per_rank": e2e_per_rank, "e2e_aggregate": e2e_aggregate(e2e_per_rank),
                           "distinct_devices_ok": devices_ok, "distinct_devices": devices_note}), flush=True)
         if not devices_ok:
             print(f"bench.py: {devices_note}", file=sys.stderr, flush=True)

@@ -71,6 +71,11 @@ def test_spawn_selftest_end_to_end(world):
     assert [p["rank"] for p in d["per_rank"]] == list(range(world))
     assert [p["local_rank"] for p in d["per_rank"]] == list(range(world))
     assert len({p["pid"] for p in d["per_rank"]}) == world  # one process per rank
+    # the N > 1 e2e leg's gather and aggregation (stand-in passes of 10 ms x (rank + 1))
+    assert len(d["e2e_per_rank"]) == world and d["e2e_aggregate"]["ranks"] == world
+    slowest = max(r["encode"]["pass_ms"] for r in d["e2e_per_rank"])
+    assert d["e2e_aggregate"]["encode"]["slowest_pass_ms"] == round(slowest, 2) >= 10 * world
+    assert d["e2e_aggregate"]["encode"]["data_GiBps"] == round(world * 1e3 / slowest, 2)
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="checks the no-GPU refusal")

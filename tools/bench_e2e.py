@@ -435,6 +435,8 @@ def main():
              "device_configs": device_configs}
     want = a.parts.split(",") if a.parts else list(parts)
     res = {name: parts[name]() for name in want}
+    from erasure_coding_test_amd import _native as N
+    res["cpu_fallbacks"] = N.fallback_count()  # the package keeps the fallback off: must be 0
     print(json.dumps(res, indent=1))
 
 

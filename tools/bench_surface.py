@@ -82,7 +82,7 @@ def main():
     rec("jerasure_schedule_encode (dumb) w=8 packetsize=4096",
         lambda: J.jerasure_schedule_encode(k, m, 8, sched, data, coding, S, 4096))
     print(json.dumps({"workload": f"RS(10,4), {a.shard_mib} MiB shards, device-resident, one stripe per call",
-                      "results": out}, indent=1))
+                      "results": out, "cpu_fallbacks": N.fallback_count()}, indent=1))
 
 
 if __name__ == "__main__":

@@ -34,6 +34,11 @@
 #include "jerasure.h"
 #include "reed_sol.h"
 
+// libecgpu.so (include/ecgpu.h): no timed call may have completed on the CPU
+// fallback; the tool turns it off and reports the count.
+extern "C" long ecgpu_fallback_count(void);
+extern "C" int ecgpu_set_knob(const char* name, int value);
+
 namespace {
 
 double now_us() {
@@ -242,7 +247,14 @@ void threads_case(const char* name, int k, int m, int size, int nthreads) {
   std::free(matrix);
 }
 
+int report_fallbacks() {
+  const long n = ecgpu_fallback_count();
+  std::printf("{\"cpu_fallbacks\": %ld}\n", n);
+  return n == 0 ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
+  ecgpu_set_knob("ECGPU_CPU_FALLBACK", 0);
   if (argc > 1 && std::strcmp(argv[1], "--threads") == 0) {
     for (int n : {1, 2, 4, 8}) {
       threads_case("C1 RS(4,2) 64 KiB", 4, 2, 64 << 10, n);
@@ -250,7 +262,7 @@ int main(int argc, char** argv) {
       threads_case("C2 RS(6,3) 1 MiB", 6, 3, 1 << 20, n);
       threads_case("C3 RS(10,4) 4 MiB", 10, 4, 4 << 20, n);
     }
-    return 0;
+    return report_fallbacks();
   }
   const bool quick = argc > 1 && std::strcmp(argv[1], "--quick") == 0;
   // --only PREFIX: the client cases whose name starts with PREFIX, stripe buffer layout only
@@ -265,7 +277,7 @@ int main(int argc, char** argv) {
   if (only) {
     for (const Case& c : cases)
       if (std::strncmp(c.name, only, std::strlen(only)) == 0) client_case(c, true, e0, 1);
-    return 0;
+    return report_fallbacks();
   }
   for (int stripe_buffer = 1; stripe_buffer >= 0; --stripe_buffer)
     for (const Case& c : cases) client_case(c, stripe_buffer != 0, e0, 1);
@@ -273,5 +285,5 @@ int main(int argc, char** argv) {
   new_pattern_case(4096);
   ecx_case(3, 3, 349525, quick ? 10 : 40);
   ecx_case(10, 4, 349525, quick ? 4 : 12);
-  return 0;
+  return report_fallbacks();
 }

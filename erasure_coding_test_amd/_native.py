@@ -1,8 +1,9 @@
 """ctypes binding of include/ecgpu.h (libecgpu.so).
 
 Loaded strictly from the in-tree build (erasure_coding_test_amd/lib/).  There
-is no fallback: if the library is missing the import fails with instructions
-to run the build.  ``torch`` is imported first on purpose -- the PyTorch-ROCm
+is no substitute for a missing library: the import fails with instructions to
+run the build.  The C library's CPU fallback on HIP errors is
+turned off for this package (PACKAGE_KNOB_DEFAULTS below).  ``torch`` is imported first on purpose -- the PyTorch-ROCm
 wheel ships its own HIP runtime (soname libamdhip64.so.7); loading it first
 makes libecgpu bind to that same runtime, so device pointers and streams from
 torch tensors are valid in our kernels.

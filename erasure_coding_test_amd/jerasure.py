@@ -6,8 +6,8 @@ tensors are used in place; CPU tensors or numpy arrays are staged through
 HBM), ``matrix`` is the flat row-major m x k coding matrix, ``erasures`` the
 erased ids (a trailing -1 is optional).  Encode/decode/dotprod run on the
 MI355X for w = 8, 16 and 32 (w = 16 / 32: size a whole number of words) and
-are synchronous; a HIP failure raises ``EcgpuError`` (there is no CPU
-fallback).  Where the reference calls exit(1) (bad w) this raises
+are synchronous; a HIP failure raises ``EcgpuError`` (the C library's CPU
+fallback is off in this package unless ECGPU_CPU_FALLBACK is set).  Where the reference calls exit(1) (bad w) this raises
 ValueError; where it returns -1 this returns -1.
 """
 from __future__ import annotations

@@ -245,8 +245,9 @@ NO_GPU = not os.path.exists("/dev/kfd")
 
 @pytest.mark.skipif(not NO_GPU, reason="checks the no-GPU failure mode")
 def test_hot_path_without_gpu_fails_loudly():
-    """No silent success and no CPU fallback: with no GPU every hot-path call
-    returns ECGPU_ERR_HIP with a message; through the drop-in names a void
+    """No silent success with the CPU fallback off (the package's and the test
+    session's setting; tests/test_cpu_fallback.py covers it on): with no GPU
+    every hot-path call returns ECGPU_ERR_HIP with a message; through the drop-in names a void
     call exits 1 with the message (the reference's convention,
     galois.cpp:330-334) and jerasure_matrix_decode returns -1 (its own
     failure result, which the client handles, client_main.cpp:2118-2124)."""

@@ -92,12 +92,6 @@ int fail_hip(hipError_t e, const char* what) {
 }
 
 
-
-ECGPU_RT_END
-
-ECGPU_RT_BEGIN
-
-
 // One non-blocking stream per device for coefficient-table uploads: a plan's
 // creation does not wait for its tables (one blocking copy cost ~12 us,
 // tools/hip_overheads.cpp); its launches wait on the upload's event instead.

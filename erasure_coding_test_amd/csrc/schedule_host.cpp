@@ -64,12 +64,13 @@ int** smart_bitmatrix_to_schedule(int k, int m, int w, const int* bitmatrix) {
     for (int i = 0; i < words; ++i) d += __builtin_popcountll(row_bits(a)[i] ^ row_bits(b)[i]);
     return d;
   };
-  std::vector<int> cost(static_cast<size_t>(rows)), base(static_cast<size_t>(rows), -1), pending;
+  std::vector<int> cost(static_cast<size_t>(rows)), base(static_cast<size_t>(rows), -1),
+      pending(static_cast<size_t>(rows));
   for (int r = 0; r < rows; ++r) {
     int pop = 0;
     for (int i = 0; i < words; ++i) pop += __builtin_popcountll(row_bits(r)[i]);
     cost[size_t(r)] = pop;
-    pending.push_back(r);
+    pending[size_t(r)] = r;
   }
   int** ops = static_cast<int**>(std::malloc(sizeof(int*) * (size_t(k) * m * w * w + 1)));
   int n = 0;

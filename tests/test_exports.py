@@ -74,7 +74,9 @@ def test_dropin_exports_reference_surface():
     assert not missing, missing
     # nothing but the reference surface leaks out (weak std:: template
     # instantiations are vague-linkage artefacts of libstdc++, not API)
-    leaked = sorted(n for n in names if not n.startswith(("galois_", "jerasure_", "reed_sol_", "std::", "__gnu")))
+    import re
+    vague = re.compile(r"^(?:[\w:<>,& ]+ )?(?:std::|__gnu)")  # a template instantiation, after its return type
+    leaked = sorted(n for n in names if not n.startswith(("galois_", "jerasure_", "reed_sol_")) and not vague.match(n))
     assert not leaked, leaked
 
 

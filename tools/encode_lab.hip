@@ -231,11 +231,37 @@ __global__ __launch_bounds__(256) void enc_sync(ApplyArgs a) {
 #pragma unroll
   for (int r = 0; r < R; ++r) store16t<1>(dp[r], col, acc[r]);
 }
+// The production body with every source load issued before any arithmetic
+// is scheduled: the source pointers are read first, then the K loads, then a
+// scheduling barrier.  In the production ISA (hipcc 7.2, gf_apply<10,4,3>)
+// the compiler issues six loads, waits for the first (vmcnt(5)) to start the
+// selector arithmetic, and issues loads 7-10 a memory latency later -- the
+// last two only after the coefficient tables' scalar loads (round 5).
+template <int K, int R, int UNITS>
+__global__ __launch_bounds__(256) void enc_sb(ApplyArgs a) {
+  const int64_t col = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (col >= a.nvec) return;
+  const int s = blockIdx.y;
+  const uint8_t* const* sp = a.src + int64_t(s) * a.src_stride;
+  const uint8_t* src[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) src[j] = sp[j];
+  uint8_t* dp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dp[r] = a.dst[int64_t(s) * a.dst_stride + a.row0 + r];
+  u32x4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = load16t<1>(src[j], col);
+  __builtin_amdgcn_sched_barrier(0);
+  combine_store<K, R, UNITS, 3, 1>(a, x, dp, col);
+}
 }  // namespace lab
 
 bool g_early0 = false;  // --early0 1: skew mode also times lab::enc_early0 on every slab
 bool g_vec2 = false;    // --vec2 1: ... and the production body with two columns per lane (VEC = 2)
 bool g_dense = false;   // --dense 1: a C4-like dense 4 x 10 map (no 0 / 1 coefficients) instead of the encode
+int g_sched = 0;        // --sched 1: production vs lab::enc_sb (all loads issued before the arithmetic)
+bool g_lost = false;    // --lost 1 (with --m 1): the lost-parity decode's map -- row 2 of the RS(k,4) Vandermonde matrix
 int g_lds = 0;          // --lds 1: the LDS nibble-table engine (production form and lab forms) beside the v_perm production;
                         // --lds 2: both engines at 3 workgroups per CU under dynamic LDS allocations of several sizes
 
@@ -300,6 +326,8 @@ int main(int argc, char** argv) {
     else if (f == "--dense") g_dense = std::atoi(argv[i + 1]) != 0;
     else if (f == "--lds") g_lds = std::atoi(argv[i + 1]);
     else if (f == "--sync") g_sync = std::atoi(argv[i + 1]);
+    else if (f == "--sched") g_sched = std::atoi(argv[i + 1]);
+    else if (f == "--lost") g_lost = std::atoi(argv[i + 1]) != 0;
     else if (f == "--skew-kib") skew_kib = std::atoi(argv[i + 1]);
     else if (f == "--skews") {
       std::string v = argv[i + 1];
@@ -323,7 +351,8 @@ int main(int argc, char** argv) {
   if (kk == 10 && mm == 4) return variant_ab<10, 4>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
   if (kk == 6 && mm == 3) return variant_ab<6, 3>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
   if (kk == 12 && mm == 4) return variant_ab<12, 4>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
-  std::fprintf(stderr, "variant A/B covers RS(10,4), RS(6,3), RS(12,4)\n");
+  if (kk == 10 && mm == 1) return variant_ab<10, 1>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
+  std::fprintf(stderr, "variant A/B covers RS(10,4), RS(6,3), RS(12,4), and (10,1) with --lost 1\n");
   return 2;
 }
 
@@ -333,6 +362,11 @@ template <int k, int m>
 int variant_ab(int stripes, size_t S, int skew_kib, int rounds, int reps) {
   const size_t stride = skew_kib >= 0 ? S + size_t(skew_kib) * 1024 : size_t(shard_stride(int64_t(S)));
   int* M = vandermonde_coding_matrix(k, m, 8);
+  if (g_lost) {  // the re-encode of a lost parity shard: row 2 of RS(k, 4), column 0 a one
+    int* M4 = vandermonde_coding_matrix(k, 4, 8);
+    for (int j = 0; j < k * m; ++j) M[j] = M4[2 * k + j % k];
+    std::free(M4);
+  }
   if (g_dense) {
     std::mt19937 gm(4);
     for (int i = 0; i < k * m; ++i) M[i] = 2 + int(gm() % 254);  // no 0 / 1: every term multiplies (C4's decode rows)
@@ -390,14 +424,26 @@ int variant_ab(int stripes, size_t S, int skew_kib, int rounds, int reps) {
   a.K = k;
   a.R = m;
   a.nt = 1;
-  constexpr int U = kUnitCol0 | kUnitRow0, N = kUnitNone;
+  constexpr int U = m == 1 ? kUnitCol0 : kUnitCol0 | kUnitRow0, N = kUnitNone;
   // bs < 0: the persistent pipelined form (a resident round of |bs| workgroups per CU)
   using V = Variant;
   const void* const vperm = reinterpret_cast<const void*>(&gf_apply<k, m, U, 1, 3, 3>);
   const void* const ldsk = reinterpret_cast<const void*>(&gf_apply_lds<k, m>);
   const int cap = k + m <= 9 ? 4 : 3;  // ecgpu_runtime.hip residency_lds_bytes
   const unsigned lds_cap = ((unsigned(163840 / cap) & ~511u) - 128u * k - 4096u) & ~4095u;
-  std::vector<Variant> vs = g_sync ? std::vector<Variant>{
+  std::vector<Variant> vs = g_sched ? (g_dense ? std::vector<Variant>{
+      V{"prod_dense_uncapped", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 0},
+      V{"sb_dense_uncapped", reinterpret_cast<const void*>(&lab::enc_sb<k, m, N>), 256, 0},
+      V{"prod_dense_cap3", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 3},
+      V{"sb_dense_cap3", reinterpret_cast<const void*>(&lab::enc_sb<k, m, N>), 256, 3},
+  } : std::vector<Variant>{
+      V{"prod", vperm, 256, cap},
+      V{"sb", reinterpret_cast<const void*>(&lab::enc_sb<k, m, U>), 256, cap},
+      V{"prod_cap_plus1", vperm, 256, cap + 1},
+      V{"sb_cap_plus1", reinterpret_cast<const void*>(&lab::enc_sb<k, m, U>), 256, cap + 1},
+      V{"prod_uncapped", vperm, 256, 0},
+      V{"sb_uncapped", reinterpret_cast<const void*>(&lab::enc_sb<k, m, U>), 256, 0},
+  }) : g_sync ? std::vector<Variant>{
       V{"prod", vperm, 256, cap},
       V{"sync_after_loads", reinterpret_cast<const void*>(&lab::enc_sync<k, m, U, 0>), 256, cap},
       V{"sync_before_stores", reinterpret_cast<const void*>(&lab::enc_sync<k, m, U, 1>), 256, cap},

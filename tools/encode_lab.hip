@@ -271,6 +271,7 @@ struct Variant {
   int bs;
   int blocks_per_cu;  // 0: uncapped
   unsigned lds = 0;   // > 0: this dynamic LDS allocation instead of the blocks_per_cu rule
+  int cols = 0;       // > 0: columns per workgroup when it is not bs (VEC > 1 forms)
 };
 
 // builds the production 3-bit-slice tables (ecgpu_runtime.hip build_tables)
@@ -352,7 +353,8 @@ int main(int argc, char** argv) {
   if (kk == 6 && mm == 3) return variant_ab<6, 3>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
   if (kk == 12 && mm == 4) return variant_ab<12, 4>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
   if (kk == 10 && mm == 1) return variant_ab<10, 1>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
-  std::fprintf(stderr, "variant A/B covers RS(10,4), RS(6,3), RS(12,4), and (10,1) with --lost 1\n");
+  if (kk == 6 && mm == 1) return variant_ab<6, 1>(stripes, size_t(kib) << 10, skew_kib, rounds, reps);
+  std::fprintf(stderr, "variant A/B covers RS(10,4), RS(6,3), RS(12,4), and (10,1) / (6,1) with --lost 1\n");
   return 2;
 }
 
@@ -431,7 +433,18 @@ int variant_ab(int stripes, size_t S, int skew_kib, int rounds, int reps) {
   const void* const ldsk = reinterpret_cast<const void*>(&gf_apply_lds<k, m>);
   const int cap = k + m <= 9 ? 4 : 3;  // ecgpu_runtime.hip residency_lds_bytes
   const unsigned lds_cap = ((unsigned(163840 / cap) & ~511u) - 128u * k - 4096u) & ~4095u;
-  std::vector<Variant> vs = g_sched ? (g_dense ? std::vector<Variant>{
+  std::vector<Variant> vs = g_sched == 2 ? std::vector<Variant>{  // the R = 1 levers (lost parity)
+      V{"prod", vperm, 256, cap},
+      V{"vec2_cap2", reinterpret_cast<const void*>(&gf_apply<k, m, U, 2, 3, 3>), 256, 2, 0, 512},
+      V{"vec2_cap3", reinterpret_cast<const void*>(&gf_apply<k, m, U, 2, 3, 3>), 256, 3, 0, 512},
+      V{"vec2_uncapped", reinterpret_cast<const void*>(&gf_apply<k, m, U, 2, 3, 3>), 256, 0, 0, 512},
+      V{"pipe_r3", reinterpret_cast<const void*>(&lab::enc_pipe<k, m, U>), -3, 0},
+      V{"pipe_r4", reinterpret_cast<const void*>(&lab::enc_pipe<k, m, U>), -4, 0},
+      V{"pipe_r6", reinterpret_cast<const void*>(&lab::enc_pipe<k, m, U>), -6, 0},
+      V{"lds_engine", ldsk, 256, cap, lds_cap},
+      V{"prod_cap2", vperm, 256, 2},
+      V{"bs512_cap2", reinterpret_cast<const void*>(&lab::enc_bs<k, m, U, 512>), 512, 2},
+  } : g_sched ? (g_dense ? std::vector<Variant>{
       V{"prod_dense_uncapped", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 0},
       V{"sb_dense_uncapped", reinterpret_cast<const void*>(&lab::enc_sb<k, m, N>), 256, 0},
       V{"prod_dense_cap3", reinterpret_cast<const void*>(&gf_apply<k, m, N, 1, 3, 3>), 256, 3},
@@ -505,7 +518,8 @@ int variant_ab(int stripes, size_t S, int skew_kib, int rounds, int reps) {
       CK(hipLaunchKernel(v.fn, dim3(unsigned(-v.bs * cus)), dim3(256), kargs, 0, nullptr));
       return;
     }
-    const dim3 grid(unsigned((a.nvec + v.bs - 1) / v.bs), unsigned(stripes));
+    const int per = v.cols > 0 ? v.cols : v.bs;
+    const dim3 grid(unsigned((a.nvec + per - 1) / per), unsigned(stripes));
     CK(hipLaunchKernel(v.fn, grid, dim3(unsigned(v.bs)), kargs, lds_of(v), nullptr));
   };
   // reference: the production launch; spot-check it against the host

@@ -760,7 +760,8 @@ def config_block(E, N, dev, stream, kind, nt, main=None):
     """Every BASELINE.json GPU config as its own launch (median of 20 HIP-event
     timed launches after warm-up; batches sized to 4.5-6.5 GB streamed per
     launch, like the timed C3 steps' 5.6 GB, so launch ramp and tail weigh
-    the same in every config): C2 encode, C3 encode / decode{0} (from the
+    the same in every config): C1's shape device-resident (RS(4,2) 64 KiB;
+    C1 itself is the reference's CPU case), C2 encode, C3 encode / decode{0} (from the
     timed steps) and its other decode shapes (`main`, c3_decode_shapes),
     C4 decode{0,1,2,3} with its host-side plan cost reported separately
     (SURVEY.md §8d), C5 encode.  Runs on every rank, on its own GPU."""
@@ -769,19 +770,24 @@ def config_block(E, N, dev, stream, kind, nt, main=None):
     import torch
     out = {}
 
-    def encode_cfg(name, k, m, S, B, cfg_id):
+    def encode_cfg(name, k, m, S, B, cfg_id, note=""):
         M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
         slab, shards = E.alloc_stripes(B, k, m, S, dev)
         fill_random(slab, list(range(B)), cfg_id)
         p = E.encode_plan(k, m, M, dev.index).bind([st[:k] for st in shards], [st[k:] for st in shards], S)
         p.set_kernel(kind, nt)
         ms = time_launches(lambda: p.launch(stream.cuda_stream), stream, CFG_REPS, warmup=CFG_WARMUP)
-        e = {"workload": f"RS({k},{m}) encode, {S >> 20} MiB shards, {B} stripes"}
+        size = f"{S >> 20} MiB" if S >= 1 << 20 else f"{S >> 10} KiB"
+        e = {"workload": f"RS({k},{m}) encode, {size} shards, {B} stripes{note}"}
         e.update(roofline_entry((k + m) * S * B, ms))
         p.close()
         out[name] = with_mix(e, xor_stream_probe(slab, S, k, m))  # after the timing: overwrites the parity
         del slab, shards
 
+    # C1 is the reference's CPU-only case (BASELINE configs[0], timed as the CPU
+    # baseline and through the drop-in); this is its shape device-resident
+    encode_cfg("C1_encode_device", 4, 2, 64 << 10, 13653, 1,
+               " (BASELINE C1's shape, device-resident; C1 itself is the CPU path)")
     encode_cfg("C2_encode", 6, 3, 1 << 20, 512, 2)
     if main is not None:
         out.update(main)

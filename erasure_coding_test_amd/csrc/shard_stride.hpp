@@ -21,6 +21,13 @@
 // (profiles/r03_skew_step_ab.jsonl); RS(12,4) 16 MiB +8 KiB (4 %).  Other
 // sizes keep +10 KiB, within 1-4 % of the best at every size measured and
 // never near a dip.
+//
+// Small shards (round 5, profiles/r05_skew_small.jsonl: 16-341 KiB at
+// RS(4,2) / RS(6,3) / RS(10,4)): up to 256 KiB NO skew is the best or within
+// 2 % of it at every size and scheme, and +10 KiB loses 4-22 % (e.g. RS(6,3)
+// 32 KiB 0.820 vs 0.670 of peak, C1's RS(4,2) 64 KiB 0.825 vs 0.747): a
+// stripe of small shards is one short contiguous run, and the skew's gaps
+// only break it up.  From ~341 KiB (the ECX block) +10 KiB is back on top.
 #pragma once
 #include <cstdint>
 
@@ -30,17 +37,20 @@ struct SkewClass {
   int64_t size, skew;
 };
 constexpr SkewClass kSkewTable[] = {
-    {256 << 10, 12 << 10}, {512 << 10, 8 << 10},  {1 << 20, 0},          {2 << 20, 12 << 10},
+    {256 << 10, 0},        {512 << 10, 8 << 10},  {1 << 20, 0},          {2 << 20, 12 << 10},
     {3 << 20, 8 << 10},    {4 << 20, 6 << 10},   {6 << 20, 12 << 10},   {8 << 20, 12 << 10},
     {12 << 20, 8 << 10},   {16 << 20, 8 << 10},   {32 << 20, 8 << 10},   {64 << 20, 8 << 10},
 };
 constexpr int64_t kDefaultSkew = 10 << 10;
+// shards up to this size (+1/16, like the table's classes) take no skew
+constexpr int64_t kNoSkewUpTo = 256 << 10;
 
-// round_up(size, 256) + the table's skew for that size (+-1/16), or
-// kDefaultSkew elsewhere.
+// round_up(size, 256) + the table's skew for that size (+-1/16), none up to
+// kNoSkewUpTo (+1/16), or kDefaultSkew elsewhere.
 inline int64_t shard_stride(int64_t size) {
   if (size < 0) size = 0;
   const int64_t rounded = (size + 255) & ~int64_t(255);
+  if (rounded <= kNoSkewUpTo + kNoSkewUpTo / 16) return rounded;
   int64_t skew = kDefaultSkew;
   for (const SkewClass& c : kSkewTable)
     if (rounded >= c.size - c.size / 16 && rounded <= c.size + c.size / 16) skew = c.skew;

@@ -179,7 +179,7 @@ def test_decode_plan_replays_reference_decode(golden, vectors):
 
 def test_recommended_stride():
     from erasure_coding_test_amd import _native as N
-    # per-size skew table (capi_host.cpp kSkewTable, profiles/r03_skew_sweep_*.jsonl), +10 KiB elsewhere
+    # per-size skew table (shard_stride.hpp kSkewTable, profiles/r03_skew_sweep_*.jsonl), +10 KiB elsewhere
     st = N.lib.ecgpu_recommended_shard_stride
     assert st(4 << 20) == (4 << 20) + (6 << 10)
     assert st((4 << 20) + 3) == (4 << 20) + 256 + (6 << 10)
@@ -187,6 +187,10 @@ def test_recommended_stride():
     assert st(1 << 20) == 1 << 20
     assert st(5 << 20) == (5 << 20) + (10 << 10)
     assert st(349525) == ((349525 + 255) & ~255) + (10 << 10)  # ECX block size
+    # round 5: no skew up to 256 KiB (+1/16), profiles/r05_skew_small.jsonl
+    for small in (1, 4096, 16 << 10, 64 << 10, 100000, 256 << 10, 272 << 10):
+        assert st(small) == (small + 255) & ~255, small
+    assert st((272 << 10) + 1) == (272 << 10) + 256 + (10 << 10)
     for size in (1, 7, 4095, 65536, (1 << 20) - 1, (3 << 20) + 17, 100 << 20):
         assert st(size) % 256 == 0 and st(size) >= size
 

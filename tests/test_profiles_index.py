@@ -33,16 +33,19 @@ def _skew_table():
     def ev(e):  # "12 << 10" -> 12288
         parts = [int(x) for x in e.split("<<")]
         return parts[0] << sum(parts[1:])
-    return {ev(a): ev(b) for a, b in re.findall(r"\{([\d <]+),\s*([\d <]+)\}", body)}
+    table = {ev(a): ev(b) for a, b in re.findall(r"\{([\d <]+),\s*([\d <]+)\}", body)}
+    no_skew = ev(re.search(r"kNoSkewUpTo = ([\d <]+);", src).group(1))
+    return table, no_skew
 
 
 def test_stride_statements_agree_with_the_table():
     """the bench's stride comment, the C header and the
     DESIGN §4 table state the skews the library actually uses."""
     import re
-    t = _skew_table()
+    t, no_skew = _skew_table()
     mib, kib = 1 << 20, 1 << 10
     assert t[4 * mib] == 6 * kib and t[16 * mib] == 8 * kib and t[1 * mib] == 0
+    assert no_skew == 256 * kib and t[no_skew] == 0  # round 5: small shards take no skew
     bench_src = open(os.path.join(ROOT, "bench.py")).read()
     assert "6 KiB at 4 MiB, 8 KiB at 16 MiB" in bench_src and "S + 10 KiB" not in bench_src
     hdr = open(os.path.join(ROOT, "include", "ecgpu.h")).read()
@@ -55,6 +58,9 @@ def test_stride_statements_agree_with_the_table():
         sz, sk = sz.strip(), sk.strip().strip("*")
         if sz == "other":
             continue
+        if sz.startswith("≤"):  # the no-skew rule's column
+            sz = sz[1:].strip()
+            assert int(sz.split()[0]) * kib == no_skew and sk == "0", (sz, sk)
         n = int(sz.split()[0]) * (kib if sz.endswith("K") else mib)
         got[n] = int(sk) * kib
     assert got == t

@@ -67,7 +67,8 @@ class StripePlan:
 def alloc_stripes(stripes: int, k: int, m: int, size: int, device=None):
     """One HBM slab for `stripes` stripes of k+m shards, laid out with the
     library's recommended shard stride (ecgpu_recommended_shard_stride: a
-    10 KiB skew so a column's k+m accesses do not share an HBM channel/bank).
+    per-size skew so a column's k+m accesses do not share an HBM channel/bank;
+    none for shards up to 256 KiB).
     Returns (slab, shards) with shards[s][i] a `size`-byte uint8 view."""
     stride = int(N.lib.ecgpu_recommended_shard_stride(size))
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)

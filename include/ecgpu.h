@@ -318,8 +318,9 @@ ECGPU_API int ecgpu_host_unregister(void* ptr);
  * `size`-byte shards: round_up(size, 256) plus a skew.  Shards at
  * power-of-two strides send a column's k+m accesses to the same HBM channel /
  * bank on different rows; the skew comes from a per-size table measured on
- * MI355X (6 KiB at 4 MiB, 8 KiB at 16 MiB, none at 1 MiB; 10 KiB for sizes
- * not in the table; shard_stride.hpp). */
+ * MI355X (6 KiB at 4 MiB, 8 KiB at 16 MiB, none at 1 MiB; none at all up to
+ * 256 KiB, where a stripe is one short contiguous run; 10 KiB for other
+ * sizes; shard_stride.hpp). */
 ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size);
 
 /* Convenience: encode `stripes` device-resident stripes with the m x k

@@ -296,6 +296,7 @@ extern "C" __attribute__((visibility("default"))) int ecgpu_diag_launch(
     if (K == 10 && R == 1) fn = &diag_xor_mix<10, 1>;
     if (K == 6 && R == 3) fn = &diag_xor_mix<6, 3>;
     if (K == 12 && R == 4) fn = &diag_xor_mix<12, 4>;
+    if (K == 4 && R == 2) fn = &diag_xor_mix<4, 2>;
   } else if (variant == 2) {
     vec = 1;
     if (K == 10 && R == 4) fn = &ecgpu::dev::gf_apply_lds<10, 4>;

@@ -22,9 +22,10 @@
 // sizes keep +10 KiB, within 1-4 % of the best at every size measured and
 // never near a dip.
 //
-// Small shards (round 5, profiles/r05_skew_small.jsonl: 16-341 KiB at
-// RS(4,2) / RS(6,3) / RS(10,4)): up to 256 KiB NO skew is the best or within
-// 2 % of it at every size and scheme, and +10 KiB loses 4-22 % (e.g. RS(6,3)
+// Small shards (round 5, profiles/r05_skew_small.jsonl: 4-341 KiB at
+// RS(4,2) / RS(6,3) / RS(10,4)): from 8 to 256 KiB NO skew is the best or
+// within 2 % of it at every size and scheme (at 4 KiB 3-5 % ahead of +10
+// KiB), and +10 KiB loses 3-22 % (e.g. RS(6,3)
 // 32 KiB 0.820 vs 0.670 of peak, C1's RS(4,2) 64 KiB 0.825 vs 0.747): a
 // stripe of small shards is one short contiguous run, and the skew's gaps
 // only break it up.  From ~341 KiB (the ECX block) +10 KiB is back on top.

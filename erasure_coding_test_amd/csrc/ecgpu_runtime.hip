@@ -266,19 +266,42 @@ std::vector<int> parse_devices(const char* s, int visible) {
   return out;
 }
 
+// Visible devices, or 0 when HIP cannot tell (no GPU: lists are not checked).
+int visible_devices() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n < 0) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  return n;
+}
+
+// The first entry of `list` that is not a visible device, or -1.
+int invisible_entry(const std::vector<int>& list, int visible) {
+  for (int d : list)
+    if (visible > 0 && d >= visible) return d;
+  return -1;
+}
+
 std::shared_ptr<const std::vector<int>> device_list() {
   static std::once_flag once;
   std::call_once(once, [] {
     const char* e = std::getenv("ECGPU_DEVICES");
     if (!e || !*e) return;
-    int n = 0;
-    if (std::strcmp(e, "all") == 0 && (hipGetDeviceCount(&n) != hipSuccess || n <= 0)) {
-      (void)hipGetLastError();
-      n = 0;
-    }
+    const int n = visible_devices();
     auto v = std::make_shared<const std::vector<int>>(parse_devices(e, n));
+    // a malformed list, or one naming a device this process cannot see, is
+    // ignored as a whole (every call would otherwise fail or fall back)
+    const int bad = invisible_entry(*v, n);
+    if (v->empty() || bad >= 0) {
+      std::fprintf(stderr, "libecgpu: ECGPU_DEVICES=\"%s\" ignored (%s)\n", e,
+                   bad >= 0 ? ("device " + std::to_string(bad) + " is not visible; " + std::to_string(n) +
+                               " visible").c_str()
+                            : "expected \"all\" or a comma-separated list of device ordinals");
+      return;
+    }
     std::lock_guard<std::mutex> lk(g_devices_mu);
-    if (!g_devices && !v->empty()) g_devices = v;
+    if (!g_devices) g_devices = v;
   });
   std::lock_guard<std::mutex> lk(g_devices_mu);
   return g_devices;
@@ -1083,6 +1106,10 @@ ECGPU_API int ecgpu_set_devices(int n, const int* devices) {
   if (n < 0 || (n > 0 && !devices)) return fail(ECGPU_ERR_ARG, "ecgpu_set_devices: bad arguments");
   for (int i = 0; i < n; ++i)
     if (devices[i] < 0) return fail(ECGPU_ERR_ARG, "ecgpu_set_devices: negative device");
+  const int visible = visible_devices();
+  if (const int bad = invisible_entry(std::vector<int>(devices, devices + n), visible); bad >= 0)
+    return fail(ECGPU_ERR_ARG, "ecgpu_set_devices: device " + std::to_string(bad) + " is not visible (" +
+                                   std::to_string(visible) + " visible)");
   (void)device_list();  // the environment's list is read first, so this call overrides it
   std::lock_guard<std::mutex> lk(g_devices_mu);
   g_devices = n > 0 ? std::make_shared<const std::vector<int>>(devices, devices + n) : nullptr;

@@ -89,7 +89,10 @@ ECGPU_API int ecgpu_device_lost(int device);
  * so concurrent callers (the reference client's byte-range encode pthreads,
  * client_main.cpp:1074-1164) each drive their own GPU.  Also read from
  * ECGPU_DEVICES ("all" or "0,1,2,..."; repeats allowed) at first use; n = 0
- * unsets.  A forced ECGPU_DEVICE wins; calls naming device memory run on the
+ * unsets.  A list naming a device HIP does not show this process is
+ * rejected (ECGPU_ERR_ARG; the environment's list is ignored with one stderr
+ * line), so a typo cannot send every call to the CPU fallback.  A forced
+ * ECGPU_DEVICE wins; calls naming device memory run on the
  * current device.  get_devices returns the list's length (0 if unset) and
  * copies up to cap entries; call_device is the device this thread's next
  * host-memory call runs on. */

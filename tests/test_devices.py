@@ -71,6 +71,35 @@ def test_set_devices_rejects_bad_arguments():
 
 # ------------------------------------------------------------------ GPU ----
 @pytest.mark.gpu
+def test_device_list_names_only_visible_devices_gpu(gpu):
+    """A list naming a device this process cannot see is rejected by
+    ecgpu_set_devices and ignored (with one stderr line) from ECGPU_DEVICES:
+    otherwise every call on it would fail or complete on the CPU."""
+    import torch
+
+    from erasure_coding_test_amd import _native as N
+    n = torch.cuda.device_count()
+    with pytest.raises(N.EcgpuError, match="not visible"):
+        N.set_devices([0, n])
+    assert N.get_devices() == []
+    N.set_devices([n - 1, 0])
+    try:
+        assert N.get_devices() == [n - 1, 0]
+    finally:
+        N.set_devices(None)
+    code = ("from erasure_coding_test_amd import _native as N\n"
+            "print(N.get_devices())\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=dict(os.environ, ECGPU_DEVICES=f"0,{n}"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == "[]"
+    assert "not visible" in r.stderr
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=dict(os.environ, ECGPU_DEVICES="all"))
+    assert r.returncode == 0 and r.stdout.strip().splitlines()[-1] == str(list(range(n))), r.stderr[-2000:]
+
+
+@pytest.mark.gpu
 def test_concurrent_pageable_encodes_over_a_device_list_gpu(gpu, restatement):
     """8 threads, each an unchanged caller's pageable RS(10,4) 4 MiB encode,
     spread over ECGPU_DEVICES = 0,0: every thread's parity bit-exact."""

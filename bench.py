@@ -949,8 +949,8 @@ def main(argv=None):
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
 
     # B stripes x (k+m) shards in one HBM slab at the library's recommended
-    # shard stride, ecgpu_recommended_shard_stride(S) = round_up(S, 256) + the
-    # skew csrc/shard_stride.hpp measured for S (6 KiB at 4 MiB, 8 KiB at 16 MiB;
+    # shard stride, ecgpu_recommended_shard_stride_km(S, k, m) = round_up(S, 256)
+    # + the skew csrc/shard_stride.hpp measured for S (6 KiB at 4 MiB, 8 KiB at 16 MiB;
     # the line records it as config.shard_stride_bytes); global stripe ids
     # round-robin over ranks
     ids = global_stripe_ids(B, rank, world)

@@ -115,6 +115,7 @@ SIGNATURES = {
     "ecgpu_plan_launch": (c_int, [c_void_p, c_void_p]),
     "ecgpu_plan_destroy": (None, [c_void_p]),
     "ecgpu_recommended_shard_stride": (c_int64, [c_int64]),
+    "ecgpu_recommended_shard_stride_km": (c_int64, [c_int64, c_int, c_int]),
     "ecgpu_pipeline_create": (c_void_p, [c_int, c_int, c_int_p, c_int64, c_int, c_int]),
     "ecgpu_pipeline_create_decode": (c_void_p, [c_int, c_int, c_int, c_int_p, c_int, c_int_p, c_int64, c_int, c_int]),
     "ecgpu_pipeline_submit": (c_int64, [c_void_p, c_void_pp, c_void_pp]),

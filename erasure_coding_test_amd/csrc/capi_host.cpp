@@ -57,15 +57,24 @@ ECGPU_API const char* ecgpu_build_id(int what) {
 }
 ECGPU_API void ecgpu_free(void* p) { std::free(p); }
 
-// The shard stride of shard_stride.hpp (the measured per-size skew table).
-ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size) {
+// The shard stride of shard_stride.hpp (the measured per-size skew table,
+// and its per-scheme entries when k + m is given).
+namespace {
+int64_t recommended_stride(int64_t size, int shards) {
   if (size < 0) size = 0;
   const int64_t rounded = (size + 255) & ~int64_t(255);
   // the shard_skew_kib knob (ECGPU_SHARD_SKEW_KIB): one skew for every size
   // (A/B runs of whole workloads); outside 0..1024 the table applies
   const int v = knob(Knob::kShardSkewKib);
   if (v >= 0 && v <= 1024) return rounded + int64_t(v) * 1024;
-  return shard_stride(size);
+  return shard_stride(size, shards);
+}
+}  // namespace
+
+ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size) { return recommended_stride(size, 0); }
+
+ECGPU_API int64_t ecgpu_recommended_shard_stride_km(int64_t size, int k, int m) {
+  return recommended_stride(size, k > 0 && m >= 0 ? k + m : 0);
 }
 
 ECGPU_API int ecgpu_galois_single_multiply(int a, int b, int w) { return single_multiply(a, b, w); }

@@ -142,7 +142,7 @@ ecgpu_pipeline* pipeline_build(int k, int m, int rows, int nsrc, const int* coef
   d.size = size;
   d.src_ids.assign(src_ids, src_ids + nsrc);
   d.out_ids.assign(out_ids, out_ids + rows);
-  d.slot_stride = size_t(ecgpu_recommended_shard_stride(size));
+  d.slot_stride = size_t(ecgpu_recommended_shard_stride_km(size, k, m));
   DeviceGuard g(d.device);
   auto bad = [&](hipError_t e, const char* what) {
     fail(ECGPU_ERR_HIP, std::string("ecgpu_pipeline: ") + what + ": " + hipGetErrorString(e));

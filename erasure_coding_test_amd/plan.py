@@ -66,11 +66,11 @@ class StripePlan:
 
 def alloc_stripes(stripes: int, k: int, m: int, size: int, device=None):
     """One HBM slab for `stripes` stripes of k+m shards, laid out with the
-    library's recommended shard stride (ecgpu_recommended_shard_stride: a
-    per-size skew so a column's k+m accesses do not share an HBM channel/bank;
-    none for shards up to 256 KiB).
+    library's recommended shard stride for the scheme
+    (ecgpu_recommended_shard_stride_km: a per-size skew so a column's k+m
+    accesses do not share an HBM channel/bank; none for small shards).
     Returns (slab, shards) with shards[s][i] a `size`-byte uint8 view."""
-    stride = int(N.lib.ecgpu_recommended_shard_stride(size))
+    stride = int(N.lib.ecgpu_recommended_shard_stride_km(size, k, m))
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     slab = torch.empty((stripes, k + m, stride), dtype=torch.uint8, device=dev)
     shards = [[slab[s, i, :size] for i in range(k + m)] for s in range(stripes)]

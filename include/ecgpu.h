@@ -321,10 +321,14 @@ ECGPU_API int ecgpu_host_unregister(void* ptr);
  * `size`-byte shards: round_up(size, 256) plus a skew.  Shards at
  * power-of-two strides send a column's k+m accesses to the same HBM channel /
  * bank on different rows; the skew comes from a per-size table measured on
- * MI355X (6 KiB at 4 MiB, 8 KiB at 16 MiB, none at 1 MiB; none at all up to
- * 256 KiB, where a stripe is one short contiguous run; 10 KiB for other
- * sizes; shard_stride.hpp). */
+ * MI355X (6 KiB at 4 MiB, 8 KiB at 16 MiB, none at 1 MiB; none up to 256 KiB,
+ * where a stripe is one short contiguous run, and at 512 KiB; 10 KiB for
+ * other sizes; shard_stride.hpp). */
 ECGPU_API int64_t ecgpu_recommended_shard_stride(int64_t size);
+/* The same for a known scheme: RS(k, m) slabs, where the measured best skew
+ * differs by scheme (RS(10,4) keeps +12 KiB at 256 KiB and +8 KiB at 512 KiB;
+ * other schemes none there).  k <= 0 = the size-only advice. */
+ECGPU_API int64_t ecgpu_recommended_shard_stride_km(int64_t size, int k, int m);
 
 /* Convenience: encode `stripes` device-resident stripes with the m x k
  * coding matrix (pointer tables are host arrays of device pointers, stripe-

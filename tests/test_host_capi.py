@@ -187,10 +187,28 @@ def test_recommended_stride():
     assert st(1 << 20) == 1 << 20
     assert st(5 << 20) == (5 << 20) + (10 << 10)
     assert st(349525) == ((349525 + 255) & ~255) + (10 << 10)  # ECX block size
-    # round 5: no skew up to 256 KiB (+1/16), profiles/r05_skew_small.jsonl
-    for small in (1, 4096, 16 << 10, 64 << 10, 100000, 256 << 10, 272 << 10):
+    # round 5: no skew up to 256 KiB (+1/16) and at 512 KiB, profiles/r05_skew_small.jsonl, r05_skew_mid.jsonl
+    for small in (1, 4096, 16 << 10, 64 << 10, 100000, 256 << 10, 272 << 10, 480 << 10, 512 << 10, 544 << 10):
         assert st(small) == (small + 255) & ~255, small
     assert st((272 << 10) + 1) == (272 << 10) + 256 + (10 << 10)
+    assert st((544 << 10) + 1) == (544 << 10) + 256 + (10 << 10)
+
+
+def test_recommended_stride_per_scheme():
+    """ecgpu_recommended_shard_stride_km: RS(10,4) (k + m = 14) keeps the
+    round-3 skews at 256 / 512 KiB; other schemes and sizes take the
+    size-only advice."""
+    from erasure_coding_test_amd import _native as N
+    km, st = N.lib.ecgpu_recommended_shard_stride_km, N.lib.ecgpu_recommended_shard_stride
+    assert km(256 << 10, 10, 4) == (256 << 10) + (12 << 10)
+    assert km(512 << 10, 10, 4) == (512 << 10) + (8 << 10)
+    assert km(500 << 10, 12, 2) == (500 << 10) + (8 << 10)  # any k + m = 14, within 1/16
+    for k, m in ((4, 2), (6, 3), (12, 4)):
+        assert km(256 << 10, k, m) == 256 << 10 and km(512 << 10, k, m) == 512 << 10
+    for size in (64 << 10, 1 << 20, 4 << 20, (4 << 20) + 3, 16 << 20, 349525):
+        for k, m in ((10, 4), (4, 2), (6, 3), (12, 4)):
+            assert km(size, k, m) == st(size), (size, k, m)
+    assert km(256 << 10, 0, 4) == st(256 << 10)  # k <= 0: the size-only advice
     for size in (1, 7, 4095, 65536, (1 << 20) - 1, (3 << 20) + 17, 100 << 20):
         assert st(size) % 256 == 0 and st(size) >= size
 
@@ -204,6 +222,7 @@ def test_stride_skew_override(knobs):
     assert st(4 << 20) == (4 << 20) + (12 << 10) and st(1 << 20) == (1 << 20) + (12 << 10)
     knobs.set("shard_skew_kib", 0)
     assert st(16 << 20) == 16 << 20
+    assert N.lib.ecgpu_recommended_shard_stride_km(512 << 10, 10, 4) == 512 << 10  # the knob wins for schemes too
     for bad in (-4, 2000):
         knobs.set("ECGPU_SHARD_SKEW_KIB", bad)
         assert st(4 << 20) == (4 << 20) + (6 << 10), bad

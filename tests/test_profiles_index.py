@@ -45,7 +45,7 @@ def test_stride_statements_agree_with_the_table():
     t, no_skew = _skew_table()
     mib, kib = 1 << 20, 1 << 10
     assert t[4 * mib] == 6 * kib and t[16 * mib] == 8 * kib and t[1 * mib] == 0
-    assert no_skew == 256 * kib and t[no_skew] == 0  # round 5: small shards take no skew
+    assert no_skew == 256 * kib and t[256 * kib] == 0 and t[512 * kib] == 0  # round 5: small shards take no skew
     bench_src = open(os.path.join(ROOT, "bench.py")).read()
     assert "6 KiB at 4 MiB, 8 KiB at 16 MiB" in bench_src and "S + 10 KiB" not in bench_src
     hdr = open(os.path.join(ROOT, "include", "ecgpu.h")).read()
@@ -58,9 +58,11 @@ def test_stride_statements_agree_with_the_table():
         sz, sk = sz.strip(), sk.strip().strip("*")
         if sz == "other":
             continue
-        if sz.startswith("≤"):  # the no-skew rule's column
+        if sz.startswith("≤"):  # the no-skew rule's column: every table class up to it
             sz = sz[1:].strip()
             assert int(sz.split()[0]) * kib == no_skew and sk == "0", (sz, sk)
+            got.update({n: 0 for n in t if n <= no_skew})
+            continue
         n = int(sz.split()[0]) * (kib if sz.endswith("K") else mib)
         got[n] = int(sk) * kib
     assert got == t

@@ -1,12 +1,13 @@
 """Small-shard stride A/B through the library (round 5): for each (k, m,
 shard size) an encode plan and a decode{0} plan bound to two slabs of the same
-stripes -- one at the library's stride (ecgpu_recommended_shard_stride: no
-skew up to 256 KiB since round 5) and one at the old +10 KiB
-(ECGPU_SHARD_SKEW_KIB=10 while it is allocated) -- timed in interleaved rounds
+stripes -- one at the library's stride for the scheme
+(ecgpu_recommended_shard_stride_km, through alloc_stripes) and one at the
+round-4 table's skew (+12 KiB at 256 KiB, +8 KiB at 512 KiB, +10 KiB at the
+other sizes here; ECGPU_SHARD_SKEW_KIB while it is allocated) -- timed in interleaved rounds
 (HIP events on the launch stream, median), ~2.5 GiB streamed per launch.
 Parity of both slabs is compared with each other after the timing.
 
-    python tools/probe_small_stride.py [--rounds 5] [--reps 10] > out.jsonl
+    python tools/probe_small_stride.py [--sizes 16,64] [--shapes '4,2;10,4'] [--rounds 5] [--reps 10] > out.jsonl
 """
 from __future__ import annotations
 
@@ -22,6 +23,7 @@ sys.path.insert(0, ROOT)
 SHAPES = [(4, 2), (6, 3), (10, 4)]
 SIZES_KIB = [16, 64, 128, 256]
 PEAK_GBS = 8000.0
+OLD_SKEW_KIB = {256: 12, 512: 8}  # the round-4 table (+10 KiB at the other sizes here)
 
 
 def main():
@@ -29,7 +31,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--gib", type=float, default=2.5)
+    ap.add_argument("--sizes", default=",".join(map(str, SIZES_KIB)), help="shard sizes, KiB")
+    ap.add_argument("--shapes", default=";".join(f"{k},{m}" for k, m in SHAPES), help="k,m;k,m;...")
     args = ap.parse_args()
+    shapes = [tuple(int(x) for x in sh.split(",")) for sh in args.shapes.split(";")]
+    sizes = [int(x) for x in args.sizes.split(",")]
     import torch
 
     import erasure_coding_test_amd as E
@@ -38,13 +44,14 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
-    for k, m in SHAPES:
+    for k, m in shapes:
         M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
-        for kib in SIZES_KIB:
+        for kib in sizes:
             S = kib << 10
             B = max(1, int(args.gib * (1 << 30)) // ((k + m) * S))
             layouts = {}
-            for name, skew in (("library", None), ("skew10", 10)):
+            old = OLD_SKEW_KIB.get(kib, 10)
+            for name, skew in (("library", None), (f"round4_skew{old}", old)):
                 if skew is not None:
                     N.set_knob("ECGPU_SHARD_SKEW_KIB", skew)
                 try:
@@ -61,7 +68,7 @@ def main():
                     L["t_enc"].append(time_launches(lambda: L["enc"].launch(stream.cuda_stream), stream, args.reps, 2))
                     L["t_dec"].append(time_launches(lambda: L["dec"].launch(stream.cuda_stream), stream, args.reps, 2))
             # the same data in both layouts?  compare parity of stripe 0 / B-1 after re-encoding from equal data
-            a, b = layouts["library"], layouts["skew10"]
+            a, b = layouts["library"], layouts[f"round4_skew{old}"]
             for s in (0, B - 1):
                 b["slab"][s, :k, :S].copy_(a["slab"][s, :k, :S])
             a["enc"].launch(stream.cuda_stream)

@@ -308,6 +308,7 @@ template <int k, int m>
 int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int reps);
 template <int k, int m>
 int variant_ab(int stripes, size_t S, int skew_kib, int rounds, int reps);
+int g_skew_unit = 1024;  // --skew-unit B: the --skews values in units of B bytes (default KiB; a multiple of 256)
 int g_sync = 0;  // --sync 1: the production body with workgroup barriers (lab::enc_sync) and the LDS engine, at the library's cap
 
 int main(int argc, char** argv) {
@@ -330,6 +331,7 @@ int main(int argc, char** argv) {
     else if (f == "--sched") g_sched = std::atoi(argv[i + 1]);
     else if (f == "--lost") g_lost = std::atoi(argv[i + 1]) != 0;
     else if (f == "--skew-kib") skew_kib = std::atoi(argv[i + 1]);
+    else if (f == "--skew-unit") g_skew_unit = std::atoi(argv[i + 1]);
     else if (f == "--skews") {
       std::string v = argv[i + 1];
       size_t p = 0;
@@ -632,7 +634,7 @@ int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int
   for (int sk : skews) {
     Slab sl{};
     sl.skew = sk;
-    sl.stride = ((S + 255) & ~size_t(255)) + size_t(sk) * 1024;
+    sl.stride = ((S + 255) & ~size_t(255)) + size_t(sk) * size_t(g_skew_unit);
     CK(hipMalloc(&sl.base, sl.stride * size_t(k + m) * size_t(stripes)));
     std::vector<const uint8_t*> hs;
     std::vector<uint8_t*> hd;
@@ -725,9 +727,10 @@ int skew_ab(int stripes, int kib, const std::vector<int>& skews, int rounds, int
   for (auto& sl : slabs) {
     std::sort(sl.t.begin(), sl.t.end());
     const double med = sl.t[sl.t.size() / 2];
-    std::printf("{\"k\": %d, \"m\": %d, \"shard_kib\": %d, \"stripes\": %d, \"skew_kib\": %d, \"median_us\": %.1f, "
-                "\"min_us\": %.1f, \"GBps\": %.0f, \"frac\": %.4f}\n",
-                k, m, kib, stripes, sl.skew, med, double(sl.t[0]), bytes / med / 1e3, bytes / med / 1e3 / 8000.0);
+    std::printf("{\"k\": %d, \"m\": %d, \"shard_kib\": %d, \"stripes\": %d, \"skew_kib\": %.2f, \"skew_bytes\": %lld, "
+                "\"median_us\": %.1f, \"min_us\": %.1f, \"GBps\": %.0f, \"frac\": %.4f}\n",
+                k, m, kib, stripes, sl.skew * double(g_skew_unit) / 1024.0, (long long)sl.skew * g_skew_unit, med,
+                double(sl.t[0]), bytes / med / 1e3, bytes / med / 1e3 / 8000.0);
     if (!g_early0) continue;
     std::sort(sl.te.begin(), sl.te.end());
     const double me = sl.te[sl.te.size() / 2];

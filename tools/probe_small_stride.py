@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--gib", type=float, default=2.5)
     ap.add_argument("--sizes", default=",".join(map(str, SIZES_KIB)), help="shard sizes, KiB")
     ap.add_argument("--shapes", default=";".join(f"{k},{m}" for k, m in SHAPES), help="k,m;k,m;...")
+    ap.add_argument("--skews", default="", help="KiB skews to time beside the library's layout instead of "
+                                                "the round-4 table's (e.g. 3,4,5,7 at 4 MiB)")
     args = ap.parse_args()
     shapes = [tuple(int(x) for x in sh.split(",")) for sh in args.shapes.split(";")]
     sizes = [int(x) for x in args.sizes.split(",")]
@@ -51,7 +53,8 @@ def main():
             B = max(1, int(args.gib * (1 << 30)) // ((k + m) * S))
             layouts = {}
             old = OLD_SKEW_KIB.get(kib, 10)
-            for name, skew in (("library", None), (f"round4_skew{old}", old)):
+            others = [(f"skew{x}", int(x)) for x in args.skews.split(",") if x] or [(f"round4_skew{old}", old)]
+            for name, skew in [("library", None)] + others:
                 if skew is not None:
                     N.set_knob("ECGPU_SHARD_SKEW_KIB", skew)
                 try:
@@ -68,23 +71,27 @@ def main():
                     L["t_enc"].append(time_launches(lambda: L["enc"].launch(stream.cuda_stream), stream, args.reps, 2))
                     L["t_dec"].append(time_launches(lambda: L["dec"].launch(stream.cuda_stream), stream, args.reps, 2))
             # the same data in both layouts?  compare parity of stripe 0 / B-1 after re-encoding from equal data
-            a, b = layouts["library"], layouts[f"round4_skew{old}"]
-            for s in (0, B - 1):
-                b["slab"][s, :k, :S].copy_(a["slab"][s, :k, :S])
-            a["enc"].launch(stream.cuda_stream)
-            b["enc"].launch(stream.cuda_stream)
-            torch.cuda.synchronize(dev)
-            same = all(torch.equal(a["slab"][s, k:, :S], b["slab"][s, k:, :S]) for s in (0, B - 1))
+            a = layouts["library"]
+            same = True
+            for name, _ in others:
+                b = layouts[name]
+                for s in (0, B - 1):
+                    b["slab"][s, :k, :S].copy_(a["slab"][s, :k, :S])
+                a["enc"].launch(stream.cuda_stream)
+                b["enc"].launch(stream.cuda_stream)
+                torch.cuda.synchronize(dev)
+                same = same and all(torch.equal(a["slab"][s, k:, :S], b["slab"][s, k:, :S]) for s in (0, B - 1))
             for name, L in layouts.items():
                 te, td = median(L["t_enc"]), median(L["t_dec"])
                 print(json.dumps({
                     "k": k, "m": m, "shard_kib": kib, "stripes": B, "layout": name, "stride": int(L["stride"]),
                     "encode_ms": round(te, 4), "encode_frac": round((k + m) * S * B / (te / 1e3) / 1e9 / PEAK_GBS, 4),
                     "decode0_ms": round(td, 4), "decode0_frac": round((k + 1) * S * B / (td / 1e3) / 1e9 / PEAK_GBS, 4),
+                    "step_ms": round(te + td, 4),
                     "parity_equal_across_layouts": bool(same)}), flush=True)
                 L["enc"].close()
                 L["dec"].close()
-            del layouts, a, b
+            del layouts, a
             torch.cuda.empty_cache()
 
 

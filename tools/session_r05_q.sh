@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-5 closing profile pass on the final tree (the scheme-aware stride and
+# C1's shape in the configs block; w = 8 kernels unchanged): kernel trace +
+# stats and the two PMC passes of the default bench command, the summary, and
+# the bench line reading this box's counters (tools/profile_round.sh).
+set -e
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r05q
+bash tools/profile_round.sh r05 > gpurun_out/r05q/profile_r05.log 2>&1
+# the raw traces exceed what gpurun copies back (64 MiB): keep the summaries
+cp gpurun_out/bench.json gpurun_out/bench.err gpurun_out/summary.log gpurun_out/r05_rocprof_summary.json \
+   gpurun_out/r05_kernel_stats.csv gpurun_out/pmc_encode.json gpurun_out/pmc_decode.json gpurun_out/r05q/
+for d in prof_trace prof_fetch prof_write; do
+  f=$(find gpurun_out/$d -name '*kernel_stats.csv' -print -quit); [ -n "$f" ] && cp "$f" gpurun_out/r05q/$d.kernel_stats.csv
+done
+rm -rf gpurun_out/prof_trace gpurun_out/prof_fetch gpurun_out/prof_write
+echo session_ok

@@ -12,7 +12,6 @@ sequential semantics (tests/test_gpu_parity.py ::test_aliased_*,
 ::test_host_region_ops_aliasing), and read-only overlaps are allowed.
 """
 import ctypes
-import os
 import random
 import subprocess
 import sys

@@ -12,7 +12,6 @@ import os
 import re
 import subprocess
 
-import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "erasure_coding_test_amd", "lib")

@@ -8,7 +8,6 @@ size-independent properties (encode -> erase -> decode round trips).
 import ctypes
 import itertools
 import os
-import random
 
 import numpy as np
 import pytest

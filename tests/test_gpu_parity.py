@@ -520,6 +520,45 @@ def test_plan_launch_is_graph_capturable(ec, gpu, restatement):
                 assert np.array_equal(shards[st][j].cpu().numpy(), hdata[st][j][:size])
 
 
+@pytest.mark.parametrize("k,m", [(4, 2), (6, 3), (10, 4), (12, 4)])
+@pytest.mark.parametrize("size", [4 << 10, (64 << 10) + 48, 256 << 10, 512 << 10])
+def test_scheme_aware_slab_round_trip(ec, gpu, restatement, k, m, size):
+    """Round 5's layouts (shard_stride.hpp: no skew up to 256 KiB and at
+    512 KiB, RS(10,4)'s own entries at 256 / 512 KiB): alloc_stripes lays the
+    slab out at ecgpu_recommended_shard_stride_km, and a batched encode, an
+    erasure of m shards and a batched decode on it are bit-exact against the
+    oracle."""
+    import torch
+
+    from erasure_coding_test_amd import _native as N
+    stripes = 3
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    slab, shards = ec.alloc_stripes(stripes, k, m, size)
+    stride = int(N.lib.ecgpu_recommended_shard_stride_km(size, k, m))
+    assert slab.stride(1) == stride and stride % 256 == 0 and stride >= size
+    hdata = [host_shards(41, st, k, size) for st in range(stripes)]
+    for st in range(stripes):
+        for j in range(k):
+            shards[st][j].copy_(torch.from_numpy(hdata[st][j][:size]))
+    ec.encode_plan(k, m, M).bind([st[:k] for st in shards], [st[k:] for st in shards], size).launch()
+    torch.cuda.synchronize()
+    refs = [_encode_ref(restatement, k, m, M, hdata[st], size) for st in range(stripes)]
+    for st in range(stripes):
+        for i in range(m):
+            assert np.array_equal(shards[st][k + i].cpu().numpy(), refs[st][i][:size]), (st, i)
+    erased = sorted(int(x) for x in np.random.default_rng(size + k).choice(k + m, size=m, replace=False))
+    for st in shards:
+        for e in erased:
+            st[e].fill_(0)
+    ec.DecodePlan(k, m, M, erased).bind_stripes(shards, size).launch()
+    torch.cuda.synchronize()
+    for st in range(stripes):
+        for j in range(k):
+            assert np.array_equal(shards[st][j].cpu().numpy(), hdata[st][j][:size]), (st, j, erased)
+        for i in range(m):
+            assert np.array_equal(shards[st][k + i].cpu().numpy(), refs[st][i][:size]), (st, i, erased)
+
+
 # --------------------------------------------------- host pipeline ----
 @pytest.mark.parametrize("memory", ["pageable", "registered", "torch_pinned"])
 def test_host_pipeline_matches_oracle(ec, gpu, restatement, memory):

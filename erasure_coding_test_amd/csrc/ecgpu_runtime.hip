@@ -227,8 +227,25 @@ int plan_bind(ecgpu_plan* p, int stripes, const uint8_t* const* src, uint8_t* co
 
 hostsync::IdlePool<Ctx> g_pool;  // idle contexts (process lifetime)
 
-int current_device() {
+int visible_devices();
+
+// A forced ECGPU_DEVICE that names a visible device (or any, when HIP cannot
+// tell), else -1: a device this process cannot see is ignored, with one
+// stderr line, instead of failing every call (or sending it to the CPU).
+int forced_device() {
   const int forced = knob(Knob::kDevice);
+  if (forced < 0) return -1;
+  static const int visible = visible_devices();
+  if (visible <= 0 || forced < visible) return forced;
+  static std::once_flag once;
+  std::call_once(once, [&] {
+    std::fprintf(stderr, "libecgpu: ECGPU_DEVICE=%d ignored (%d visible)\n", forced, visible);
+  });
+  return -1;
+}
+
+int current_device() {
+  const int forced = forced_device();
   if (forced >= 0) return forced;
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess) d = 0;
@@ -311,7 +328,7 @@ std::shared_ptr<const std::vector<int>> device_list() {
 // ECGPU_DEVICE, else this thread's device from the ECGPU_DEVICES list, else
 // the caller's current device.
 int host_call_device() {
-  if (knob(Knob::kDevice) >= 0) return knob(Knob::kDevice);
+  if (const int forced = forced_device(); forced >= 0) return forced;
   const auto list = device_list();
   if (!list || list->empty()) return current_device();
   thread_local std::shared_ptr<const std::vector<int>> t_list;
@@ -327,7 +344,7 @@ int host_call_device() {
 // as before: classify() rejects another device's buffers); an all-host call
 // takes host_call_device().
 int call_device(const std::vector<void*>& a, const std::vector<void*>& b) {
-  if (knob(Knob::kDevice) >= 0) return knob(Knob::kDevice);
+  if (const int forced = forced_device(); forced >= 0) return forced;
   const auto list = device_list();
   if (!list || list->empty()) return current_device();
   if (any_device_buffer(a) || any_device_buffer(b)) return current_device();
@@ -1011,7 +1028,7 @@ int execute_split(const FusedOp& op, int64_t size, int ways, int ndev, const cha
   // range i's device: a forced ECGPU_DEVICE keeps every range on it (N
   // contexts there); an ECGPU_DEVICES list is walked from this thread's entry;
   // otherwise every visible device in turn from the current one
-  const int forced = knob(Knob::kDevice);
+  const int forced = forced_device();
   const auto list = device_list();
   size_t list_pos = 0;
   if (forced < 0 && list && !list->empty()) {

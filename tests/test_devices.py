@@ -97,6 +97,13 @@ def test_device_list_names_only_visible_devices_gpu(gpu):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=ROOT,
                        env=dict(os.environ, ECGPU_DEVICES="all"))
     assert r.returncode == 0 and r.stdout.strip().splitlines()[-1] == str(list(range(n))), r.stderr[-2000:]
+    # a forced ECGPU_DEVICE the process cannot see is ignored the same way
+    code = ("from erasure_coding_test_amd import _native as N\n"
+            "print(N.lib.ecgpu_call_device())\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=dict(os.environ, ECGPU_DEVICE=str(n)))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == "0" and f"ECGPU_DEVICE={n} ignored" in r.stderr
 
 
 @pytest.mark.gpu

@@ -2,8 +2,9 @@
 
 Loaded strictly from the in-tree build (erasure_coding_test_amd/lib/).  There
 is no substitute for a missing library: the import fails with instructions to
-run the build.  The C library's CPU fallback on HIP errors is
-turned off for this package (PACKAGE_KNOB_DEFAULTS below).  ``torch`` is imported first on purpose -- the PyTorch-ROCm
+run the build.  The C library's CPU fallback on HIP errors and
+its CPU executor for small host-memory calls are turned off for this package
+(PACKAGE_KNOB_DEFAULTS below).  ``torch`` is imported first on purpose -- the PyTorch-ROCm
 wheel ships its own HIP runtime (soname libamdhip64.so.7); loading it first
 makes libecgpu bind to that same runtime, so device pointers and streams from
 torch tensors are valid in our kernels.
@@ -46,6 +47,7 @@ SIGNATURES = {
     "ecgpu_get_knob": (c_int, [c_char_p, c_int_p]),
     "ecgpu_free": (None, [c_void_p]),
     "ecgpu_fallback_count": (c_int64, []),
+    "ecgpu_cpu_call_count": (c_int64, []),
     "ecgpu_device_lost": (c_int, [c_int]),
     "ecgpu_set_devices": (c_int, [c_int, c_int_p]),
     "ecgpu_get_devices": (c_int, [c_int_p, c_int]),
@@ -159,7 +161,11 @@ class EcgpuError(RuntimeError):
 # keeps running; this package -- what the tests, smoke() and bench.py drive --
 # fails loudly instead (EcgpuError), so no checked or measured result can come
 # from the CPU.  An ECGPU_CPU_FALLBACK set in the environment wins.
-PACKAGE_KNOB_DEFAULTS = {"ECGPU_CPU_FALLBACK": 0}
+#
+# ECGPU_MIN_OFFLOAD_KIB: the C library runs small host-memory calls on its CPU
+# executor (below the measured crossover); this package sends
+# every call to the GPU, so each checked or measured result is the HIP path's.
+PACKAGE_KNOB_DEFAULTS = {"ECGPU_CPU_FALLBACK": 0, "ECGPU_MIN_OFFLOAD_KIB": 0}
 
 
 def _apply_package_defaults(names=None) -> None:
@@ -202,6 +208,12 @@ def get_devices() -> list:
 def fallback_count() -> int:
     """Synchronous calls completed on the CPU after a HIP error (ecgpu_fallback_count)."""
     return int(lib.ecgpu_fallback_count())
+
+
+def cpu_call_count() -> int:
+    """Synchronous host-memory calls run on the CPU executor by choice
+    (ECGPU_MIN_OFFLOAD_KIB / ECGPU_GPU=0; ecgpu_cpu_call_count)."""
+    return int(lib.ecgpu_cpu_call_count())
 
 
 def get_knob(name: str) -> int:

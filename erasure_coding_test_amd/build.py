@@ -42,13 +42,13 @@ HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 
 HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp", "contract_host.cpp", "knobs.cpp",
-             "cpu_fallback.cpp"]
+             "cpu_fallback.cpp", "cpu_exec.cpp"]
 # (source, object, extra flags): the specialised kernel table is split into
 # one translation unit per output-row count so the four compile in parallel
 HIP_UNITS = [(f, f + ".o", []) for f in ("ecgpu_runtime.hip", "dispatch_w8.hip", "dispatch_wide.hip", "accum.hip",
                                            "pipeline.hip", "packets.hip")] + [
     (f"{t}.hip", f"{t}_r{r}.hip.o", [f"-DECGPU_SPEC_R={r}"]) for t in ("gf_spec", "wide_spec") for r in (1, 2, 3, 4)]
-HDRS = ["buffer_contract.hpp", "cpu_fallback.hpp", "gf_host.hpp", "knobs.hpp", "shard_stride.hpp", "host_sync.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp", "gf_kernels_w8.hpp", "gf_kernels_wide.hpp",
+HDRS = ["buffer_contract.hpp", "cpu_fallback.hpp", "cpu_exec.hpp", "gf_host.hpp", "knobs.hpp", "shard_stride.hpp", "host_sync.hpp", "matrix_host.hpp", "planner.hpp", "schedule_host.hpp", "gf_kernels.hpp", "gf_kernels_w8.hpp", "gf_kernels_wide.hpp",
         "gf_kernels_packets.hpp", "gf_spec.hpp", "wide_spec.hpp", "diag_kernels_w8.hpp",
         "runtime.hpp"]
 DROPIN_SRCS = ["jerasure_dropin.cpp", "jerasure_surface.cpp"]

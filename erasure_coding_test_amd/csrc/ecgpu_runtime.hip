@@ -60,14 +60,15 @@ ECGPU_RT_BEGIN
 // Errors after which the device's context is unusable for the rest of the
 // process (a kernel fault, a lost / missing device or driver): the device is
 // marked lost, and with ECGPU_CPU_FALLBACK later synchronous calls on it go
-// straight to the CPU (cpu_fallback.hpp).
+// straight to the CPU (cpu_fallback.hpp).  hipErrorInvalidDevice is not one:
+// a bad ordinal argument returns it (ecgpu_device_pci_bus_id(99)) on a
+// healthy device.
 bool sticky(hipError_t e) {
   switch (e) {
     case hipErrorNotInitialized:
     case hipErrorDeinitialized:
     case hipErrorInsufficientDriver:
     case hipErrorNoDevice:
-    case hipErrorInvalidDevice:
     case hipErrorNoBinaryForGpu:
     case hipErrorECCNotCorrectable:
     case hipErrorIllegalAddress:
@@ -75,20 +76,34 @@ bool sticky(hipError_t e) {
     case hipErrorContextIsDestroyed:
     case hipErrorAssert:
     case hipErrorLaunchFailure:
-    case hipErrorUnknown:
       return true;
     default:
       return false;
   }
 }
 
+// The device the current synchronous call targets (CallDeviceScope), -1
+// outside one.
+thread_local int t_call_device = -1;
+
+CallDeviceScope::CallDeviceScope(int device) : prev(t_call_device) { t_call_device = device; }
+CallDeviceScope::~CallDeviceScope() { t_call_device = prev; }
+
 int fail_hip(hipError_t e, const char* what) {
-  if (sticky(e)) {
-    int d = 0;
-    if (hipGetDevice(&d) != hipSuccess) d = 0;
-    mark_device_lost(d);
+  std::string msg = std::string(what) + ": " + hipGetErrorString(e);
+  int d = t_call_device;
+  if (d < 0 && hipGetDevice(&d) != hipSuccess) d = -1;
+  bool lost = sticky(e);
+  if (!lost && e == hipErrorUnknown && d >= 0) {
+    // ordinary failures return it too: sticky only when the device still
+    // fails a synchronize afterwards
+    DeviceGuard g(d);
+    (void)hipGetLastError();
+    lost = hipDeviceSynchronize() != hipSuccess;
+    (void)hipGetLastError();
   }
-  return fail(ECGPU_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  if (lost && d >= 0) mark_device_lost(d);
+  return fail(ECGPU_ERR_HIP, msg);
 }
 
 
@@ -347,7 +362,7 @@ int call_device(const std::vector<void*>& a, const std::vector<void*>& b) {
   if (const int forced = forced_device(); forced >= 0) return forced;
   const auto list = device_list();
   if (!list || list->empty()) return current_device();
-  if (any_device_buffer(a) || any_device_buffer(b)) return current_device();
+  if (!all_host(a) || !all_host(b)) return current_device();
   return host_call_device();
 }
 
@@ -728,11 +743,14 @@ int map_buffers(const FusedOp& op, int64_t size, int device, bool inl, CallMap* 
 }
 
 // The call is about to write caller memory (a D2H or host copy into an
-// output, or a kernel writing an output in place): from here on a failure
-// cannot be completed on the CPU (cpu_fallback.hpp).  Also the test
-// injection's "after the first write" failure point.
-int caller_write_point(int device) {
-  note_caller_write();
+// output, or a kernel writing an output in place).  The fused map reads its
+// sources only, so a partly written output is recomputed whole by the CPU
+// executor -- unless some output is also a source, whose original bytes are
+// then gone: from here on such a call cannot be completed on the CPU
+// (cpu_fallback.hpp).  Also the test injection's "after the first write"
+// failure point.
+int caller_write_point(const FusedOp& op, int device) {
+  if (op.dst_is_src) note_caller_write();
   return injected_failure(device, 1);
 }
 
@@ -761,9 +779,9 @@ int exec_zero_copy(Ctx* c, const FusedOp& op, CallMap& m) {
   for (int j = 0; j < m.nsrc; ++j)
     if (m.staged[size_t(j)]) std::memcpy(m.devp[size_t(j)], op.srcs[size_t(j)], size_t(m.size));
   if (writes_in_place(op, m))
-    if (int rc = caller_write_point(c->device)) return rc;
+    if (int rc = caller_write_point(op, c->device)) return rc;
   if (int rc = launch_and_sync(c, op, m, /*host_io=*/true)) return rc;
-  if (int rc = caller_write_point(c->device)) return rc;
+  if (int rc = caller_write_point(op, c->device)) return rc;
   for (int r = 0; r < m.rows; ++r) {
     const size_t i = m.index(op.dsts[size_t(r)]);
     if (m.staged[i]) std::memcpy(op.dsts[size_t(r)], m.devp[i], size_t(m.size));
@@ -806,9 +824,9 @@ int exec_outputs_zero_copy(Ctx* c, const FusedOp& op, CallMap& m, bool* done) {
   }
   if (int rc = copy_shards(true, c->stage, m.slot, staged_hp, size_t(m.size), c->stream)) return rc;
   if (writes_in_place(op, m))
-    if (int rc = caller_write_point(c->device)) return rc;
+    if (int rc = caller_write_point(op, c->device)) return rc;
   if (int rc = launch_and_sync(c, op, m, /*host_io=*/true)) return rc;
-  if (int rc = caller_write_point(c->device)) return rc;
+  if (int rc = caller_write_point(op, c->device)) return rc;
   for (size_t i = 0; i < m.bufs.size(); ++i)
     if (m.staged[i] && is_out[i]) std::memcpy(m.bufs[i], m.devp[i], size_t(m.size));
   *done = true;
@@ -852,7 +870,7 @@ int exec_staged(Ctx* c, const FusedOp& op, CallMap& m, bool inl) {
   if (via_temp)
     for (int r = 0; r < rows; ++r) dp[size_t(r)] = c->stage + (m.nstage + size_t(r)) * slot;
   if (writes_in_place(op, m))
-    if (int rc = caller_write_point(c->device)) return rc;
+    if (int rc = caller_write_point(op, c->device)) return rc;
   if (nsrc == 0) {
     // Every output is identically zero (e.g. region multiply by 0 without
     // add, galois.cpp:447-451): nothing to read.
@@ -888,13 +906,13 @@ int exec_staged(Ctx* c, const FusedOp& op, CallMap& m, bool inl) {
     ECGPU_HIP(hipStreamSynchronize(c->stream));
     ECGPU_HIP(hipGetLastError());
     if (!outs.empty())
-      if (int rc = caller_write_point(c->device)) return rc;
+      if (int rc = caller_write_point(op, c->device)) return rc;
     for (const auto& o : outs) std::memcpy(o.second, c->bounce + (o.first - c->stage), size);
     return ECGPU_OK;
   }
   // from here the D2H copies write the caller's outputs directly
   if (!outs.empty())
-    if (int rc = caller_write_point(c->device)) return rc;
+    if (int rc = caller_write_point(op, c->device)) return rc;
   // outputs in consecutive slots: one 2-D copy per evenly spaced run of host outputs
   bool consecutive = true;
   for (size_t i = 1; i < outs.size() && consecutive; ++i) consecutive = outs[i].first == outs[0].first + i * slot;
@@ -921,48 +939,64 @@ int execute_on_gpu(const FusedOp& op, int64_t size, int device) {
   DeviceGuard g(device);
   const bool inl = inline_ok(op, size);
   CallMap m;
-  if (int rc = map_buffers(op, size, device, inl, &m)) return rc;
-  if (int rc = injected_failure(device, 0)) return rc;
-  if (inl && m.nstage > 0 && m.nstage * size_t(size) <= zc_max()) return exec_zero_copy(c, op, m);
-  if (inl && m.nstage > 0 && m.nstage * m.slot > bounce_max()) {
+  int rc = map_buffers(op, size, device, inl, &m);
+  if (rc == ECGPU_OK) rc = injected_failure(device, 0);
+  if (rc == ECGPU_OK) {
     bool done = false;
-    if (int rc = exec_outputs_zero_copy(c, op, m, &done)) return rc;
-    if (done) return ECGPU_OK;
-  }
-  return exec_staged(c, op, m, inl);
-}
-
-// Is any buffer device (or managed) memory -- a call the CPU cannot complete?
-bool any_device_buffer(const std::vector<void*>& bufs) {
-  for (void* p : bufs) {
-    hipPointerAttribute_t attr;
-    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-      (void)hipGetLastError();  // unregistered pageable memory (or no HIP at all)
-      continue;
+    if (inl && m.nstage > 0 && m.nstage * size_t(size) <= zc_max()) {
+      rc = exec_zero_copy(c, op, m);
+      done = true;
+    } else if (inl && m.nstage > 0 && m.nstage * m.slot > bounce_max()) {
+      rc = exec_outputs_zero_copy(c, op, m, &done);
     }
-    if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) return true;
+    if (rc == ECGPU_OK && !done) rc = exec_staged(c, op, m, inl);
   }
-  return false;
+  // a failure returns with nothing of the call still in flight: a launch or
+  // copy queued before the failing step no longer writes caller memory
+  // behind the CPU executor's back (cpu_fallback.hpp)
+  if (rc != ECGPU_OK) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipGetLastError();
+  }
+  return rc;
 }
 
-bool any_device_buffer(const FusedOp& op) {
-  return any_device_buffer(op.srcs) || any_device_buffer(op.dsts);
+Where where(const void* p) {
+  hipPointerAttribute_t attr;
+  const hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e == hipSuccess)
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged ? Where::kDevice : Where::kHost;
+  (void)hipGetLastError();
+  // unregistered pageable memory, or no GPU runtime at all (then no device
+  // memory can exist); any other failure proves nothing
+  return e == hipErrorInvalidValue || e == hipErrorNoDevice || e == hipErrorInsufficientDriver ? Where::kHost
+                                                                                                : Where::kUnknown;
 }
+
+bool all_host(const std::vector<void*>& bufs) {
+  for (void* p : bufs)
+    if (where(p) != Where::kHost) return false;
+  return true;
+}
+
+bool all_host(const FusedOp& op) { return all_host(op.srcs) && all_host(op.dsts); }
 
 // execute_on_gpu under SURVEY §8b's failure contract (cpu_fallback.hpp): a
-// HIP error before any caller byte was written, on a call whose buffers are
-// all host memory, completes on the CPU (ECGPU_CPU_FALLBACK, default on);
-// a device marked lost by a sticky error sends such calls straight there.
+// HIP error on a call whose buffers are all host memory, before it wrote a
+// source (an output that is also one), completes on the CPU
+// (ECGPU_CPU_FALLBACK, default on); a device marked lost by a sticky error
+// sends such calls straight there.
 int execute_on(const FusedOp& op, int64_t size, int device, const char* call) {
   trace_begin();
+  CallDeviceScope scope(device);
   const bool fallback = fallback_enabled();
-  if (fallback && device_lost(device) && !any_device_buffer(op)) {
+  if (fallback && device_lost(device) && all_host(op)) {
     record_fallback(call, "device " + std::to_string(device) + " marked lost by an earlier HIP error");
     cpu_apply(op, size);
     return ECGPU_OK;
   }
   const int rc = execute_on_gpu(op, size, device);
-  if (rc != ECGPU_ERR_HIP || !fallback || caller_written() || any_device_buffer(op)) return rc;
+  if (rc != ECGPU_ERR_HIP || !fallback || caller_written() || !all_host(op)) return rc;
   record_fallback(call, "HIP error: " + t_err);
   cpu_apply(op, size);
   t_err = std::string(call) + ": completed on the CPU after a HIP error: " + t_err;
@@ -997,19 +1031,7 @@ int split_ways(const FusedOp& op, int64_t size, int* ndev) {
   const int per_device = list && !list->empty() ? int(list->size()) : n;  // -1: one range per listed / visible device
   const int ways = int(std::min<int64_t>(v < 0 ? per_device : v, size / min_bytes));
   if (ways <= 1) return 1;
-  auto on_host = [](const void* p) {
-    hipPointerAttribute_t attr;
-    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-      (void)hipGetLastError();
-      return true;  // unregistered pageable memory
-    }
-    return attr.type != hipMemoryTypeDevice && attr.type != hipMemoryTypeManaged;
-  };
-  for (void* p : op.srcs)
-    if (!on_host(p)) return 1;
-  for (void* p : op.dsts)
-    if (!on_host(p)) return 1;
-  return ways;
+  return all_host(op) ? ways : 1;
 }
 
 FusedOp shifted(const FusedOp& op, int64_t off) {
@@ -1063,6 +1085,14 @@ int execute_split(const FusedOp& op, int64_t size, int ways, int ndev, const cha
   return ECGPU_OK;
 }
 
+// Distinct buffers x size: the bytes a call reads and writes once each.
+int64_t bytes_moved(const FusedOp& op, int64_t size) {
+  size_t n = op.srcs.size();
+  for (void* d : op.dsts)
+    if (std::find(op.srcs.begin(), op.srcs.end(), d) == op.srcs.end()) ++n;
+  return int64_t(n) * size;
+}
+
 // A synchronous call over `size` bytes of every buffer of the fused op.
 int execute(const FusedOp& op, int64_t size, const char* call) {
   if (op.w != 8 && size % (op.w / 8) != 0)
@@ -1071,6 +1101,14 @@ int execute(const FusedOp& op, int64_t size, const char* call) {
   if (int rc = check_op_buffers(call, op, size)) return rc;
   add_stats(op);
   if (op.dsts.empty() || size <= 0) return ECGPU_OK;
+  // small host-memory calls (and all of them with ECGPU_GPU=0) on the CPU
+  // executor: below the crossover the GPU round trip costs more than the
+  // arithmetic (cpu_fallback.hpp)
+  if (cpu_by_choice(bytes_moved(op, size)) && all_host(op)) {
+    record_cpu_call();
+    cpu_apply(op, size);
+    return ECGPU_OK;
+  }
   int ndev = 1;
   const int ways = split_ways(op, size, &ndev);
   if (ways > 1) return execute_split(op, size, ways, ndev, call);

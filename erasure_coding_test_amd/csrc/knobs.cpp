@@ -19,9 +19,10 @@ int fail(int code, const std::string& msg);  // capi_host.cpp
 namespace {
 
 struct KnobDef {
-  const char* env;  // environment variable (nullptr: settable only through ecgpu_set_knob)
+  const char* env;  // the knob's long name (ECGPU_*), read from the environment unless set_only
   const char* name;
   int dflt;
+  bool set_only = false;  // settable only through ecgpu_set_knob (test hooks: never from a deployment's environment)
 };
 
 // Defaults are the production choices (measured).
@@ -52,7 +53,10 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_SPLIT_MIN_KIB", "split_min_kib", 1024},
     {nullptr, "test_d2h_delay_us", 0},
     {"ECGPU_CPU_FALLBACK", "cpu_fallback", 1},
-    {"ECGPU_TEST_INJECT_HIP", "test_inject_hip", 0},
+    {"ECGPU_TEST_INJECT_HIP", "test_inject_hip", 0, true},
+    {"ECGPU_GPU", "gpu", 1},
+    {"ECGPU_MIN_OFFLOAD_KIB", "min_offload_kib", 1024},
+    {"ECGPU_CPU_SIMD", "cpu_simd", -1},
 };
 
 constexpr int kUnset = INT_MIN;
@@ -62,7 +66,7 @@ std::atomic<int> g_over[int(Knob::kCount)];   // ecgpu_set_knob's value, kUnset 
 
 // A whole-string decimal integer, else the default (so "", "x", "12k" keep it).
 int parse_env(const KnobDef& d) {
-  const char* e = d.env ? std::getenv(d.env) : nullptr;
+  const char* e = d.env && !d.set_only ? std::getenv(d.env) : nullptr;
   if (!e || !*e) return d.dflt;
   errno = 0;
   char* end = nullptr;

@@ -43,8 +43,14 @@ enum class Knob : int {
                     // worker sleeps this long before issuing a job (widens a race window)
   kCpuFallback,     // ECGPU_CPU_FALLBACK: a synchronous host-memory call that hits a HIP error before
                     // writing caller memory completes on the CPU (cpu_fallback.hpp), 1 on (default), 0 off
-  kTestInjectHip,   // ECGPU_TEST_INJECT_HIP (tests only): synchronous calls fail with ECGPU_ERR_HIP, 1 before
-                    // the first launch, 2 the same and the device marked lost, 3 after writing caller memory
+  kTestInjectHip,   // test_inject_hip (tests only, ecgpu_set_knob; never read from the environment):
+                    // synchronous calls fail with ECGPU_ERR_HIP, 1 before the first launch, 2 the same and
+                    // the device marked lost, 3 after writing caller memory
+  kGpu,             // ECGPU_GPU: 0 runs every synchronous host-memory call on the CPU executor (cpu_exec.hpp)
+  kMinOffloadKib,   // ECGPU_MIN_OFFLOAD_KIB: a synchronous host-memory call moving fewer bytes (distinct
+                    // buffers x size) runs on the CPU executor; 0 = every call on the GPU
+  kCpuSimd,         // ECGPU_CPU_SIMD: the CPU executor's SIMD level, -1 the host's best, 2 AVX-512 + GFNI,
+                    // 1 AVX2, 0 scalar (never above what the host has)
   kCount
 };
 

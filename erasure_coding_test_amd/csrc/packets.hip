@@ -96,35 +96,59 @@ int execute_packets(const FusedOp& op, const std::vector<char*>& ptrs, int64_t n
   add_stats(op);
   std::vector<void*> slot_ptrs;
   for (int sl : slots) slot_ptrs.push_back(ptrs[size_t(sl)]);
+  // small host-memory calls (and all of them with ECGPU_GPU=0) on the CPU
+  // executor, as for the w = 8 calls (execute)
+  int64_t moved = 0;
+  for (int sl : slots) moved += extent[size_t(sl)];
+  if (cpu_by_choice(moved) && all_host(slot_ptrs)) {
+    record_cpu_call();
+    cpu_apply_packets(op, ptrs, nsp, spstride, ps);
+    return ECGPU_OK;
+  }
   const int device = call_device(slot_ptrs, {});
   // SURVEY §8b's failure contract, as for the w = 8 calls (cpu_fallback.hpp):
   // host-memory calls complete on the CPU after a HIP error that came before
-  // any caller byte was written, or at once on a device marked lost
+  // a source was overwritten, or at once on a device marked lost
   trace_begin();
+  CallDeviceScope scope(device);
   const bool fallback = fallback_enabled();
-  if (fallback && device_lost(device) && !any_device_buffer(slot_ptrs)) {
+  if (fallback && device_lost(device) && all_host(slot_ptrs)) {
     record_fallback(call, "device " + std::to_string(device) + " marked lost by an earlier HIP error");
     cpu_apply_packets(op, ptrs, nsp, spstride, ps);
     return ECGPU_OK;
   }
   const int rc = execute_packets_gpu(op, ptrs, nsp, spstride, ps, device, slots, extent, is_out);
-  if (rc != ECGPU_ERR_HIP || !fallback || caller_written() || any_device_buffer(slot_ptrs)) return rc;
+  if (rc != ECGPU_ERR_HIP || !fallback || caller_written() || !all_host(slot_ptrs)) return rc;
   record_fallback(call, "HIP error: " + t_err);
   cpu_apply_packets(op, ptrs, nsp, spstride, ps);
   t_err = std::string(call) + ": completed on the CPU after a HIP error: " + t_err;
   return ECGPU_OK;
 }
 
+int packets_on_ctx(Ctx* c, const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride,
+                   int64_t ps, int device, const std::vector<int>& slots, const std::vector<int64_t>& extent,
+                   const std::vector<char>& is_out);
+
 // The GPU part of execute_packets: staging, one launch per 32 output rows,
-// the copies back.
+// the copies back.  A failure returns with nothing of the call in flight.
 int execute_packets_gpu(const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride, int64_t ps,
                         int device, const std::vector<int>& slots, const std::vector<int64_t>& extent,
                         const std::vector<char>& is_out) {
-  const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
   CtxLease lease(device);
   if (!lease.c) return lease.rc;
-  Ctx* c = lease.c;
   DeviceGuard g(device);
+  const int rc = packets_on_ctx(lease.c, op, ptrs, nsp, spstride, ps, device, slots, extent, is_out);
+  if (rc != ECGPU_OK) {
+    (void)hipStreamSynchronize(lease.c->stream);
+    (void)hipGetLastError();
+  }
+  return rc;
+}
+
+int packets_on_ctx(Ctx* c, const FusedOp& op, const std::vector<char*>& ptrs, int64_t nsp, int64_t spstride,
+                   int64_t ps, int device, const std::vector<int>& slots, const std::vector<int64_t>& extent,
+                   const std::vector<char>& is_out) {
+  const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size());
   const bool via_temp = op.dst_is_src && rows > kPacketRows;
   const int ngroups = (rows + kPacketRows - 1) / kPacketRows;
 
@@ -253,7 +277,10 @@ int execute_packets_gpu(const FusedOp& op, const std::vector<char*>& ptrs, int64
       ECGPU_HIP(hipMemcpy2DAsync(real, size_t(nsp > 1 ? spstride : ps), db[size_t(r)], size_t(ps), size_t(ps),
                                  size_t(nsp), hipMemcpyDeviceToDevice, c->stream));
     }
-  note_caller_write();  // the launches above wrote device slots in place; the copies below write host ones
+  // the launches above wrote device slots in place; the copies below write
+  // host ones (a slot's packets that are not outputs come back unchanged):
+  // only an output that is also a source loses bytes the CPU would need
+  if (op.dst_is_src) note_caller_write();
   if (int rc = injected_failure(device, 1)) return rc;
   for (int sl : slots)
     if (staged[size_t(sl)] && is_out[size_t(sl)])

@@ -66,8 +66,26 @@ int fail(int code, const std::string& msg);  // knobs: knobs.hpp
 
 // A HIP failure: ECGPU_ERR_HIP with the message; an error that leaves the
 // device's context unusable (sticky: a kernel fault, a lost or missing
-// device) also marks the current device lost (cpu_fallback.hpp).
+// device) also marks the device lost (cpu_fallback.hpp) -- the device the
+// current synchronous call targets (CallDeviceScope), else the current one.
 int fail_hip(hipError_t e, const char* what);
+
+// Names the device a synchronous call runs on for fail_hip, for its lifetime.
+struct CallDeviceScope {
+  int prev;
+  explicit CallDeviceScope(int device);
+  ~CallDeviceScope();
+  CallDeviceScope(const CallDeviceScope&) = delete;
+  CallDeviceScope& operator=(const CallDeviceScope&) = delete;
+};
+
+// Where a buffer lives: host memory (pageable, pinned or registered), device
+// (or managed) memory, or unknown (the pointer query failed for a reason that
+// does not prove host memory -- e.g. a sticky error; the CPU must not touch it).
+enum class Where { kHost, kDevice, kUnknown };
+Where where(const void* p);
+// Every buffer host memory, positively known (the CPU executor may run the call).
+bool all_host(const std::vector<void*>& bufs);
 
 #define ECGPU_HIP(expr)                                 \
   do {                                                  \
@@ -181,8 +199,5 @@ int launch_inline(const FusedOp& op, const std::vector<const uint8_t*>& sp, cons
 // Runs a fused op synchronously; `call` names the entry point in errors
 // (e.g. a buffer-contract rejection, buffer_contract.hpp).
 int execute(const FusedOp& op, int64_t size, const char* call = "ecgpu");
-// Is any of these buffers device (or managed) memory -- a call the CPU
-// fallback cannot complete (cpu_fallback.hpp)?
-bool any_device_buffer(const std::vector<void*>& bufs);
 
 ECGPU_RT_END

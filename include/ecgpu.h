@@ -18,14 +18,19 @@
  * star), 16 or 32 (wide-word kernels; size a whole number of w/8-byte words,
  * else ECGPU_ERR_ARG) and so do the w16/w32 region functions.  These accept host OR device pointers
  * (classified per buffer; host buffers are staged through HBM) and are
- * synchronous: results are valid on return, like the reference.  A HIP
- * failure on a call whose buffers are all host memory, before any byte of
- * them was written, completes on the CPU (no new failure modes;
- * counted by ecgpu_fallback_count, the first one logged on stderr) unless the
+ * synchronous: results are valid on return, like the reference.  A call
+ * whose buffers are all host memory and that moves fewer than
+ * ECGPU_MIN_OFFLOAD_KIB bytes (distinct buffers x size; every such call with
+ * ECGPU_GPU=0) runs on the library's own CPU executor, where the GPU round
+ * trip would cost more (counted by ecgpu_cpu_call_count).  A HIP failure on
+ * a call whose buffers are all host memory, before it overwrote one of its
+ * sources, completes on the CPU (no new failure modes; counted
+ * by ecgpu_fallback_count, the first one logged on stderr) unless the
  * ECGPU_CPU_FALLBACK knob is 0; any other HIP failure returns ECGPU_ERR_HIP
  * (through the void-returning drop-in names: exits with a message).  The
- * Python package turns the fallback off unless the environment sets the
- * knob, and the bench and tests assert the count is 0.  Buffers of one
+ * Python package turns the fallback off and the threshold to 0 unless the
+ * environment sets them, and the bench and tests assert both counts are 0.
+ * Buffers of one
  * call are identical or disjoint: a written region that partially overlaps
  * another region of the call returns ECGPU_ERR_ARG before anything runs
  * (see ecgpu_plan_check_buffers).
@@ -83,6 +88,9 @@ ECGPU_API void ecgpu_free(void* p);                    /* == free()           */
  * host-memory calls on it run on the CPU without touching it. */
 ECGPU_API int64_t ecgpu_fallback_count(void);
 ECGPU_API int ecgpu_device_lost(int device);
+/* Synchronous host-memory calls run on the CPU executor by choice: below
+ * ECGPU_MIN_OFFLOAD_KIB, or with ECGPU_GPU=0 (process total). */
+ECGPU_API int64_t ecgpu_cpu_call_count(void);
 /* The devices synchronous host-memory calls spread over (default: unset, the
  * caller's current device).  Each calling thread is given one entry,
  * round-robin in the order threads make their first such call, and keeps it,

@@ -14,10 +14,16 @@ for p in (ROOT, TESTS):
 GOLDEN_DIR = os.path.join(TESTS, "golden")
 REFERENCE_ROOT = "/root/reference"
 
-# No test result may come from the drop-in's CPU fallback (SURVEY §8b,
-# csrc/cpu_fallback.hpp): off for this process and every process a test
-# starts, unless the test sets it itself (tests/test_cpu_fallback.py).
+# No test result may come from the library's CPU executor (csrc/cpu_exec.hpp):
+# neither the fallback after a HIP error nor the small-call
+# routing below ECGPU_MIN_OFFLOAD_KIB -- both off for this process and every
+# process a test starts, unless the test sets them itself
+# (tests/test_cpu_fallback.py, tests/test_cpu_exec.py).  ECGPU_TEST_INJECT_HIP
+# is the drivers' own variable (the library never reads it; they set the
+# test_inject_hip knob from it).
 os.environ["ECGPU_CPU_FALLBACK"] = "0"
+os.environ["ECGPU_MIN_OFFLOAD_KIB"] = "0"
+os.environ.pop("ECGPU_GPU", None)
 os.environ.pop("ECGPU_TEST_INJECT_HIP", None)
 
 
@@ -85,9 +91,11 @@ def knobs():
 
 @pytest.fixture(autouse=True)
 def _no_cpu_fallback():
-    """Every test ends with ecgpu_fallback_count() == 0 in this process: a GPU
-    result that silently came from the CPU would void the parity claims."""
+    """Every test ends with ecgpu_fallback_count() == ecgpu_cpu_call_count() ==
+    0 in this process: a GPU result that silently came from the CPU would void
+    the parity claims."""
     yield
     N = sys.modules.get("erasure_coding_test_amd._native")
     if N is not None:
         assert N.fallback_count() == 0, "a synchronous call completed on the CPU fallback inside the test session"
+        assert N.cpu_call_count() == 0, "a synchronous call ran on the CPU executor inside the test session"

@@ -3,9 +3,11 @@ the reference's own callers' call sequences through libjerasure_amd.so's
 C++-mangled names, checked against golden fixtures and the reference built
 here (oracle/_ref, as the checker).
 
-    python tests/fallback_driver.py client|ecx|surface
+    python tests/fallback_driver.py client|ecx|surface|pinned|pinned_alias|oom
 
-Run with ECGPU_TEST_INJECT_HIP / ECGPU_CPU_FALLBACK in the environment; prints
+Run with ECGPU_TEST_INJECT_HIP (this driver's variable: it sets the library's
+test-only test_inject_hip knob, which no deployment's environment can) and
+ECGPU_CPU_FALLBACK in the environment; prints
 one JSON line {"scenario", "checked", "mismatches", "fallbacks", "lost"} and
 exits 0 when every output matched (the drop-in itself exits 1 where a call
 cannot complete).  No torch: the drop-in is loaded the way an unchanged C++
@@ -24,6 +26,12 @@ caller loads it.
 * surface -- the rest of the header surface on the fallback: w = 16 / 32
   region multiplies and matrix encode, dot products, bit-matrix and schedule
   encode, RAID-6, against the reference (-fno-strict-aliasing build for w = 16).
+* pinned / pinned_alias -- registered host buffers the kernel writes in place:
+  an encode (outputs identical to no source: recoverable after a partial
+  write) and an in-place region multiply (the output is the source: not).
+* oom -- GPU only: HBM filled by hipMalloc until it fails, then the client's
+  C3 4 MiB encode + decode{0,1,2,3}: the library's staging hipMalloc fails for
+  real.
 """
 from __future__ import annotations
 
@@ -255,11 +263,105 @@ def surface(d, ref, ref_nsa, run):
     run.check(np.array_equal(a, b), "in-place region multiply")
 
 
+def set_injection(core):
+    """ECGPU_TEST_INJECT_HIP -> the library's test_inject_hip knob."""
+    v = int(os.environ.get("ECGPU_TEST_INJECT_HIP", "0") or 0)
+    if v:
+        core.ecgpu_set_knob.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        assert core.ecgpu_set_knob(b"test_inject_hip", v) == 0
+
+
+def register(core, arrays):
+    """hipHostRegister each array (ecgpu_host_register): pinned host memory
+    the kernels read and write in place."""
+    core.ecgpu_host_register.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    for a in arrays:
+        assert core.ecgpu_host_register(a.ctypes.data, a.nbytes) == 0
+
+
+def pinned(d, ref, core, run):
+    """RS(6,3) 1 MiB encode on registered (pinned) buffers: the inline kernel
+    writes the coding shards in place over PCIe, so a failure after that
+    point has partly written caller memory -- recoverable, since no output is
+    also a source (the map reads the sources only)."""
+    k, m, size = 6, 3, 1 << 20
+    M = matrix(d, k, m)
+    data = shards(2, 0, k, size, pad=0)
+    coding = [np.full(size, 0xA5, np.uint8) for _ in range(m)]
+    register(core, data + coding)
+    d["encode"](k, m, 8, ints(M), ptrs(data), ptrs(coding), size)
+    want = [np.zeros(size, np.uint8) for _ in range(m)]
+    ref["encode"](k, m, 8, ints(M), ptrs(data), ptrs(want), size)
+    for i in range(m):
+        run.check(np.array_equal(coding[i], want[i]), f"pinned encode coding {i}")
+
+
+def pinned_alias(d, ref, core, run):
+    """In-place region multiply (r2 = NULL, galois.cpp:429) of a registered
+    buffer: the output IS the source, so once the kernel started writing it
+    the CPU can no longer recompute it -- the call keeps the error."""
+    size = 1 << 20
+    buf = np.random.default_rng(3).integers(0, 256, size, dtype=np.uint8)
+    want = buf.copy()
+    register(core, [buf])
+    d["rmul8"](buf.ctypes.data, 77, size, None, 0)
+    ref["rmul8"](want.ctypes.data, 77, size, None, 0)
+    run.check(np.array_equal(buf, want), "pinned in-place region multiply")
+
+
+def fill_hbm(hip):
+    """Allocates device memory until hipMalloc fails (HBM exhausted), so the
+    library's own staging hipMalloc fails for real (SURVEY §8b's contract on
+    a genuine HIP error, not an injected one).  Returns the byte count held."""
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMemGetInfo.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+    free, total = ctypes.c_size_t(), ctypes.c_size_t()
+    assert hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) == 0
+    held, keep = 0, []
+    chunk = max(free.value - (256 << 20), 1 << 20)
+    while chunk >= (1 << 20):
+        p = ctypes.c_void_p()
+        if hip.hipMalloc(ctypes.byref(p), chunk) == 0:
+            keep.append(p)
+            held += chunk
+        else:
+            hip.hipGetLastError()
+            chunk //= 4
+    return held, keep
+
+
+def oom(d, core, golden, run):
+    """The client's C3 calls (client_main.cpp:1060, :2118) on one malloc'd
+    stripe buffer with HBM full: every staging hipMalloc fails."""
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime libecgpu.so is bound to (already loaded)
+    held, keep = fill_hbm(hip)
+    run.held = held
+    k, m, size = 10, 4, 4 << 20
+    M = matrix(d, k, m)
+    slab = np.zeros((k + m) * size, np.uint8)
+    sh = [slab[i * size:(i + 1) * size] for i in range(k + m)]
+    for i in range(k):
+        sh[i][:] = splitmix_bytes(size, shard_seed(3, 0, i))
+    d["encode"](k, m, 8, ints(M), ptrs(sh[:k]), ptrs(sh[k:]), size)
+    run.check([fnv1a64(c) for c in sh[k:]] == golden["full_size"]["C3"]["coding"], "C3 4 MiB encode digests (HBM full)")
+    keep_data = [s.copy() for s in sh[:4]]
+    for s in sh[:4]:
+        s[:] = 0xEE
+    rc = d["decode"](k, m, 8, ints(M), 0, ints([0, 1, 2, 3, -1]), ptrs(sh[:k]), ptrs(sh[k:]), size)
+    run.check(rc == 0 and all(np.array_equal(a, b) for a, b in zip(sh[:4], keep_data)),
+              "C3 4 MiB decode{0,1,2,3} (HBM full)")
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    for p in keep:
+        hip.hipFree(p)
+
+
 def main():
     scenario = sys.argv[1]
     with open(os.path.join(TESTS, "golden", "golden.json")) as fh:
         golden = json.load(fh)
     d = bind(os.path.join(LIB, "libjerasure_amd.so"))
+    core = ctypes.CDLL(os.path.join(LIB, "libecgpu.so"))  # the instance the drop-in links
+    set_injection(core)
     run = Run(scenario)
     if scenario == "client":
         client(d, golden, run)
@@ -268,13 +370,20 @@ def main():
     elif scenario == "surface":
         surface(d, bind(os.path.join(REF, "libjerasure_ref.so")), bind(os.path.join(REF, "libjerasure_ref_nsa.so")),
                 run)
+    elif scenario == "pinned":
+        pinned(d, bind(os.path.join(REF, "libjerasure_ref.so")), core, run)
+    elif scenario == "pinned_alias":
+        pinned_alias(d, bind(os.path.join(REF, "libjerasure_ref.so")), core, run)
+    elif scenario == "oom":
+        oom(d, core, golden, run)
     else:
         raise SystemExit(f"unknown scenario {scenario}")
-    core = ctypes.CDLL(os.path.join(LIB, "libecgpu.so"))
     core.ecgpu_fallback_count.restype = ctypes.c_int64
+    core.ecgpu_cpu_call_count.restype = ctypes.c_int64
     core.ecgpu_device_lost.restype = ctypes.c_int
     print(json.dumps({"scenario": scenario, "checked": run.checked, "mismatches": run.mismatches[:20],
-                      "fallbacks": int(core.ecgpu_fallback_count()), "lost": int(core.ecgpu_device_lost(0))}),
+                      "fallbacks": int(core.ecgpu_fallback_count()), "cpu_calls": int(core.ecgpu_cpu_call_count()),
+                      "lost": int(core.ecgpu_device_lost(0)), "hbm_held": getattr(run, "held", None)}),
           flush=True)
     return 0 if not run.mismatches else 3
 

@@ -6,7 +6,9 @@ too), dot products with and without src_ids, region multiply / XOR -- at
 sizes in whole 8-byte words up to 256 KiB, a quarter of them with buffers
 repeated inside the call (identical pointers: the reference's sequential
 semantics).  Run by tests/test_cpu_fallback.py with ECGPU_CPU_FALLBACK=1 and
-ECGPU_TEST_INJECT_HIP set, so every call completes on the CPU.
+ECGPU_TEST_INJECT_HIP set, so every call completes on the CPU, and by
+tests/test_cpu_exec.py with ECGPU_GPU=0 (every call on the CPU executor by
+choice) at each ECGPU_CPU_SIMD level.
 
     python tests/fallback_fuzz.py [cases] [seed]     -> one JSON line, exit 0 if all matched
 """
@@ -23,7 +25,7 @@ TESTS = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(TESTS)
 sys.path.insert(0, TESTS)
 sys.path.insert(0, ROOT)
-from fallback_driver import LIB, REF, bind, ints, matrix, ptrs  # noqa: E402
+from fallback_driver import LIB, REF, bind, ints, matrix, ptrs, set_injection  # noqa: E402
 
 SIZES = [8, 24, 4096, 4104, 65536, 100000, 262144]
 
@@ -33,6 +35,8 @@ def main():
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 20261017
     d = bind(os.path.join(LIB, "libjerasure_amd.so"))
     r = bind(os.path.join(REF, "libjerasure_ref.so"))
+    core = ctypes.CDLL(os.path.join(LIB, "libecgpu.so"))
+    set_injection(core)
     rng = np.random.default_rng(seed)
     bad, kinds = [], {"encode": 0, "decode": 0, "dotprod": 0, "region": 0, "aliased": 0}
     for case in range(cases):
@@ -104,10 +108,11 @@ def main():
                 outs.append((x, y, z))
             if not all(np.array_equal(p, q) for p, q in zip(*outs)):
                 bad.append((case, kind, op, c, size))
-    core = ctypes.CDLL(os.path.join(LIB, "libecgpu.so"))
     core.ecgpu_fallback_count.restype = ctypes.c_int64
+    core.ecgpu_cpu_call_count.restype = ctypes.c_int64
     print(json.dumps({"cases": cases, "kinds": kinds, "mismatches": [str(b) for b in bad[:10]],
-                      "fallbacks": int(core.ecgpu_fallback_count())}), flush=True)
+                      "fallbacks": int(core.ecgpu_fallback_count()), "cpu_calls": int(core.ecgpu_cpu_call_count())}),
+          flush=True)
     return 0 if not bad else 3
 
 

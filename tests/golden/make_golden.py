@@ -170,6 +170,23 @@ def main():
                            "data": [fnv1a64(x[:size]) for x in data], "coding": [fnv1a64(x[:size]) for x in coding]}
     g["full_size"] = full
 
+    # ---- 8b. C4 at its BASELINE size on INCONSISTENT inputs --------------
+    # RS(10,4) 4 MiB shards whose parity is NOT the data's: the reference's
+    # survivor choice (dm_ids = the first k non-erased, jerasure.cpp:84-112),
+    # its row_k_ones shortcut and the re-encode of erased parity from the
+    # RECOVERED data (:223-247) all show in the bytes, at the size whose
+    # launches differ from the 1000-B cases' (plan / batched path).
+    k, m, size = 10, 4, 4 << 20
+    M = ref.vandermonde_coding_matrix(k, m)
+    c4 = []
+    for erasures, rko in (([0, 1, 2, 3], 0), ([0, 1, 2, 3], 1), ([12], 0), ([1, 4, 11, 13], 0), ([2, 10], 1)):
+        data = shards_from_seeds(4, 7, k, size)
+        coding = shards_from_seeds(4, 7, m, size, first=k)  # NOT a codeword on purpose
+        rc = ref.matrix_decode(k, m, M, rko, erasures, data, coding, size)
+        c4.append({"erasures": erasures, "row_k_ones": rko, "rc": rc, "stripe": 7,
+                   "digests": [fnv1a64(x[:size]) for x in data + coding]})
+    g["c4_full_inconsistent"] = {"k": k, "m": m, "size": size, "cfg": 4, "cases": c4}
+
     # ---- 9. stats semantics (jerasure.cpp:1143-1151 fill order) ----------
     ref.get_stats()
     k, m = 10, 4

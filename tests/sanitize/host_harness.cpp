@@ -190,9 +190,10 @@ void cpu_fallback_exec(unsigned seed) {
     seed = seed * 1103515245u + 12345u;
     return seed >> 8;
   };
-  for (int trial = 0; trial < 24; ++trial) {
+  for (int trial = 0; trial < 72; ++trial) {
     const int w = trial % 3 == 0 ? 8 : trial % 3 == 1 ? 16 : 32;
-    const int nbuf = 2 + int(rnd() % 4);
+    const int level = (trial / 3) % 3;  // scalar, AVX2, AVX-512 + GFNI (capped at the host's)
+    const int nbuf = 2 + int(rnd() % 8);  // up to 9 buffers: > 4 output rows, aliased ones included
     const size_t n = size_t(w / 8) * (1 + rnd() % ((70u << 10) / unsigned(w / 8)));
     const uint32_t mask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
     std::vector<std::vector<uint8_t>> seq(static_cast<size_t>(nbuf)), fused;
@@ -204,7 +205,7 @@ void cpu_fallback_exec(unsigned seed) {
     LinearTracker t(w);
     std::vector<void*> id(static_cast<size_t>(nbuf));
     for (int i = 0; i < nbuf; ++i) id[size_t(i)] = fused[size_t(i)].data();
-    const int nops = 1 + int(rnd() % 6);
+    const int nops = 1 + int(rnd() % 12);
     for (int o = 0; o < nops; ++o) {
       const int a = int(rnd() % unsigned(nbuf)), b = int(rnd() % unsigned(nbuf)), c = int(rnd() % unsigned(nbuf));
       const int kind = int(rnd() % 3);
@@ -229,7 +230,7 @@ void cpu_fallback_exec(unsigned seed) {
         t.mul(id[size_t(a)], int(k), id[size_t(b)], add);
       }
     }
-    ecgpu::rt::cpu_apply(t.finish(), int64_t(n));
+    ecgpu::rt::cpu_apply(t.finish(), int64_t(n), level);
     for (int i = 0; i < nbuf; ++i) expect(fused[size_t(i)] == seq[size_t(i)], "cpu_apply vs sequential", trial, i);
   }
   // packets: slots x rows of ps bytes, super-packets nsp apart
@@ -257,7 +258,7 @@ void cpu_fallback_exec(unsigned seed) {
     }
     std::vector<char*> ptrs;
     for (auto& b : fused) ptrs.push_back(b.data());
-    ecgpu::rt::cpu_apply_packets(t.finish(), ptrs, nsp, spstride, ps);
+    ecgpu::rt::cpu_apply_packets(t.finish(), ptrs, nsp, spstride, ps, trial % 3);
     for (int i = 0; i < nslots; ++i) expect(fused[size_t(i)] == seq[size_t(i)], "cpu_apply_packets", trial, i);
   }
   // the bookkeeping, concurrently under TSan
@@ -270,6 +271,13 @@ void cpu_fallback_exec(unsigned seed) {
   expect(ecgpu::rt::caller_written(), "caller write noted");
   ecgpu::rt::mark_device_lost(5);
   expect(ecgpu_device_lost(5) == 1 && ecgpu_device_lost(4) == 0, "device lost bits");
+  // ordinals past 63 have their own flags; out-of-range ones are never lost
+  ecgpu::rt::mark_device_lost(700);
+  ecgpu::rt::mark_device_lost(-1);
+  ecgpu::rt::mark_device_lost(5000);
+  expect(ecgpu_device_lost(700) == 1 && ecgpu_device_lost(63) == 0 && ecgpu_device_lost(0) == 0 &&
+             ecgpu_device_lost(-1) == 0 && ecgpu_device_lost(5000) == 0,
+         "device lost flags per ordinal");
 }
 
 void run_all() {

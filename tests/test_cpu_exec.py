@@ -1,0 +1,215 @@
+"""The library's CPU executor for small synchronous host-memory calls
+(csrc/cpu_exec.hpp, csrc/cpu_fallback.hpp; SURVEY.md §5 "min offload size",
+§7 "the fallback for tiny sizes").
+
+A synchronous call whose buffers are all host memory and that moves fewer than
+ECGPU_MIN_OFFLOAD_KIB bytes (distinct buffers x size) runs on the calling
+thread's CPU -- vgf2p8affineqb on AVX-512 + GFNI hosts, the nibble split on
+AVX2, else scalar -- because below the measured crossover the GPU round trip
+costs more than the arithmetic.  ECGPU_GPU=0 sends every such
+call there.  It is the library's own code: nothing from oracle/ or the
+reference, which serve here only as the checkers.
+
+The reference's own call sequences (tests/fallback_driver.py: the client's
+encode / decode, the ECX datanode's per-block region ops, the rest of the
+header surface) run in subprocesses through the C++-mangled names at every
+SIMD level, against the golden fixtures and the reference built in
+oracle/_ref; a 1,500-case fuzz per level against the reference.  The
+Python package, the bench and the rest of the suite keep the threshold at 0
+(tests/conftest.py asserts ecgpu_cpu_call_count() == 0 after every test).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "tests", "fallback_driver.py")
+FUZZ = os.path.join(ROOT, "tests", "fallback_fuzz.py")
+LEVELS = [0, 1, 2]  # scalar, AVX2, AVX-512 + GFNI (capped at what the host has)
+
+
+def _need_reference():
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libjerasure_ref.so")):
+        import refcheck
+        refcheck.reference_missing("oracle/_ref/libjerasure_ref.so")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("ECGPU_GPU", "ECGPU_MIN_OFFLOAD_KIB", "ECGPU_CPU_SIMD", "ECGPU_TEST_INJECT_HIP")}
+    env["ECGPU_CPU_FALLBACK"] = "0"  # nothing may reach the CPU through the fallback here
+    env.update({k: str(v) for k, v in kw.items()})
+    return env
+
+
+def drive(scenario, timeout=600, **kw):
+    r = subprocess.run([sys.executable, DRIVER, scenario], capture_output=True, text=True, timeout=timeout,
+                       env=_env(**kw), cwd=ROOT)
+    out = None
+    for line in r.stdout.splitlines():
+        if line.startswith("{"):
+            out = json.loads(line)
+    return r, out
+
+
+def run_py(code, timeout=300, **kw):
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout,
+                          env=_env(**kw), cwd=ROOT)
+
+
+# ------------------------------------------------------------------ CPU ----
+@pytest.mark.parametrize("level", LEVELS)
+@pytest.mark.parametrize("scenario", ["client", "ecx", "surface"])
+def test_cpu_executor_reference_sequences(scenario, level):
+    """ECGPU_GPU=0: every call of the reference's sequences on the CPU executor
+    by choice, bit-exact, none through the fallback (here any GPU attempt would
+    fail -- no device, fallback off -- and the drop-in would exit 1)."""
+    _need_reference()
+    r, out = drive(scenario, ECGPU_GPU=0, ECGPU_CPU_SIMD=level)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert out["mismatches"] == [] and out["checked"] > 0, out
+    assert out["fallbacks"] == 0 and out["cpu_calls"] > 0, out
+
+
+@pytest.mark.parametrize("level", LEVELS)
+def test_cpu_executor_fuzz_vs_reference(level):
+    """1,500 random synchronous calls (encode k 1..20 x m 1..8, decodes of up to
+    m + 1 erasures with return codes, dot products, region ops, a quarter with
+    repeated buffers) on the CPU executor, equal to the compiled reference."""
+    _need_reference()
+    r = subprocess.run([sys.executable, FUZZ, "1500", str(4000 + level)], capture_output=True, text=True, timeout=600,
+                       env=_env(ECGPU_GPU=0, ECGPU_CPU_SIMD=level), cwd=ROOT)
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert out["mismatches"] == [] and out["fallbacks"] == 0 and out["cpu_calls"] >= 1350, out  # decodes that return -1 never execute
+
+
+def test_min_offload_threshold_boundary():
+    """A call moving fewer than the threshold's bytes runs on the CPU; one
+    moving exactly that many goes to the GPU (here: no device, fallback off, so
+    it fails -- which shows it was not run on the CPU)."""
+    code = ("import numpy as np\n"
+            "from erasure_coding_test_amd import _native as N, galois as G\n"
+            "N.set_knob('ECGPU_MIN_OFFLOAD_KIB', 1)\n"  # 1024 bytes
+            "a = np.arange(512, dtype=np.uint8); b = a[::-1].copy(); c = np.zeros(512, np.uint8)\n"
+            "G.galois_region_xor(a, b, c, 511)\n"  # r1, r2, r3 distinct: 3 x 511 = 1533 >= 1024 -> GPU
+            "print('unexpected')\n")
+    r = run_py(code)
+    assert "unexpected" not in r.stdout and r.returncode != 0, (r.stdout, r.stderr[-2000:])
+    code = ("import numpy as np\n"
+            "from erasure_coding_test_amd import _native as N, galois as G\n"
+            "N.set_knob('ECGPU_MIN_OFFLOAD_KIB', 1)\n"
+            "a = np.arange(512, dtype=np.uint8); b = a[::-1].copy(); c = np.zeros(512, np.uint8)\n"
+            "G.galois_region_xor(a, b, c, 341)\n"  # 3 x 341 = 1023 < 1024 -> CPU
+            "assert np.array_equal(c[:341], a[:341] ^ b[:341]) and not c[341:].any()\n"
+            "G.galois_region_xor(a, b, b, 511)\n"  # r3 == r2: 2 distinct x 511 = 1022 -> CPU
+            "assert np.array_equal(b[:511], (a ^ a[::-1])[:511]) and b[511] == 0\n"
+            "print('cpu_calls', N.cpu_call_count(), 'fallbacks', N.fallback_count())\n")
+    r = run_py(code)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "cpu_calls 2 fallbacks 0" in r.stdout, r.stdout
+
+
+def test_ecx_block_sequence_below_default_threshold():
+    """The unchanged ECX datanode's per-block calls (349,525-B blocks, 2
+    distinct buffers each) fall under the library's default threshold: with
+    the GPU untouched and the fallback off they complete, bit-exact."""
+    _need_reference()
+    code = ("from erasure_coding_test_amd import _native as N\n"
+            "import ctypes; v = ctypes.c_int(); N.lib.ecgpu_reset_knob(b'ECGPU_MIN_OFFLOAD_KIB')\n"
+            "N.lib.ecgpu_get_knob(b'ECGPU_MIN_OFFLOAD_KIB', ctypes.byref(v)); print(v.value)\n")
+    r = run_py(code)
+    default_kib = int(r.stdout.split()[-1])
+    assert default_kib > 0, "the library's default threshold must be a measured crossover, not 0"
+    r, out = drive("ecx")
+    if 2 * 349525 < default_kib * 1024:
+        assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+        assert out["mismatches"] == [] and out["fallbacks"] == 0 and out["cpu_calls"] > 0, out
+
+
+def test_gpu_switch_does_not_touch_device_memory_logic():
+    """ECGPU_GPU=0 is a routing switch for host memory only: the package's
+    knob defaults keep it on, and a reset restores them."""
+    code = ("from erasure_coding_test_amd import _native as N\n"
+            "assert N.get_knob('ECGPU_GPU') == 1 and N.get_knob('ECGPU_MIN_OFFLOAD_KIB') == 0\n"
+            "N.set_knob('ECGPU_MIN_OFFLOAD_KIB', 64); N.reset_knob('min_offload_kib')\n"
+            "assert N.get_knob('ECGPU_MIN_OFFLOAD_KIB') == 0\n"
+            "print('ok')\n")
+    r = run_py(code)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_injection_knob_is_not_read_from_the_environment():
+    """a stray ECGPU_TEST_INJECT_HIP in a deployed datanode's
+    environment must not fail calls -- the hook is settable only in-process."""
+    code = ("from erasure_coding_test_amd import _native as N\n"
+            "print('inject', N.get_knob('test_inject_hip'))\n")
+    r = run_py(code, ECGPU_TEST_INJECT_HIP=2)
+    assert r.returncode == 0 and "inject 0" in r.stdout, (r.stdout, r.stderr[-2000:])
+
+
+def test_bad_device_ordinal_does_not_mark_a_device_lost():
+    """ecgpu_device_pci_bus_id(999) fails (invalid or no device) but
+    leaves device 0 usable (a fresh process: in this one, earlier no-device
+    calls may have marked it lost on purpose)."""
+    code = ("import ctypes\n"
+            "from erasure_coding_test_amd import _native as N\n"
+            "buf = ctypes.create_string_buffer(64)\n"
+            "assert N.lib.ecgpu_device_pci_bus_id(999, buf, 64) == N.ECGPU_ERR_HIP\n"
+            "print('lost', N.lib.ecgpu_device_lost(0))\n")
+    r = run_py(code)
+    assert r.returncode == 0 and "lost 0" in r.stdout, (r.stdout, r.stderr[-2000:])
+
+
+# ------------------------------------------------------------------ GPU ----
+@pytest.mark.gpu
+def test_default_threshold_client_sequence_gpu():
+    """The library's defaults on the MI355X: the client's small calls (C1-C3
+    golden stripes at 1-4 KiB, the golden inconsistent decodes) run on the CPU
+    executor, its C3 4 MiB stripe on the GPU; every byte as the reference's."""
+    _need_reference()
+    r, out = drive("client")
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert out["mismatches"] == [] and out["fallbacks"] == 0, out
+    assert 0 < out["cpu_calls"] < out["checked"], out  # some, not all (C3 4 MiB stays on the GPU)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scenario", ["client", "ecx", "surface"])
+def test_gpu_switch_off_gpu(scenario):
+    _need_reference()
+    r, out = drive(scenario, ECGPU_GPU=0)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert out["mismatches"] == [] and out["fallbacks"] == 0 and out["cpu_calls"] > 0, out
+
+
+@pytest.mark.gpu
+def test_device_buffers_ignore_the_cpu_routing_gpu(gpu, knobs):
+    """Device memory never runs on the CPU executor, whatever the knobs say."""
+    import numpy as np
+    import torch
+
+    from erasure_coding_test_amd import _native as N, jerasure as J, reed_sol as R
+    k, m, size = 4, 2, 4096
+    M = R.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    d = [torch.full((size,), i + 1, dtype=torch.uint8, device=gpu) for i in range(k)]
+    c = [torch.zeros(size, dtype=torch.uint8, device=gpu) for _ in range(m)]
+    knobs.set("ECGPU_GPU", 0)
+    knobs.set("ECGPU_MIN_OFFLOAD_KIB", 1 << 20)
+    J.jerasure_matrix_encode(k, m, 8, M, d, c, size)
+    assert N.cpu_call_count() == 0
+    assert np.array_equal(c[0].cpu().numpy(), np.full(size, 1 ^ 2 ^ 3 ^ 4, np.uint8))
+
+
+@pytest.mark.gpu
+def test_bad_device_ordinal_does_not_mark_a_device_lost_gpu(gpu):
+    import ctypes
+
+    from erasure_coding_test_amd import _native as N
+    buf = ctypes.create_string_buffer(64)
+    assert N.lib.ecgpu_device_pci_bus_id(99, buf, 64) == N.ECGPU_ERR_HIP
+    assert N.lib.ecgpu_device_lost(0) == 0
+    assert N.lib.ecgpu_device_pci_bus_id(0, buf, 64) == 0

@@ -80,6 +80,52 @@ def test_decode_inconsistent_golden(ec, gpu, golden):
         assert digests(to_host(bufs), size) == case["digests"], (case["erasures"], case["row_k_ones"])
 
 
+@pytest.fixture(scope="module")
+def c4_inputs(golden):
+    """The C4 stripe of golden["c4_full_inconsistent"]: 14 x 4 MiB shards whose
+    parity is NOT the data's (host, pageable)."""
+    g = golden["c4_full_inconsistent"]
+    k, m, size, cfg = g["k"], g["m"], g["size"], g["cfg"]
+    return host_shards(cfg, 7, k, size) + host_shards(cfg, 7, m, size, first=k)
+
+
+@pytest.mark.parametrize("path", ["sync-device", "sync-host", "plan-2-stripes"])
+def test_c4_full_size_inconsistent_golden(ec, gpu, golden, c4_inputs, path):
+    """BASELINE config 4 at its own size (RS(10,4), 4 MiB shards) on inputs that
+    are not a codeword, against the reference's jerasure_matrix_decode digests:
+    the survivor choice (dm_ids = the first k non-erased, jerasure.cpp:84-112),
+    the row_k_ones shortcut and the re-encode of erased parity from the
+    recovered data (:223-247) show in the bytes.  Through the synchronous call
+    on device and on pageable host buffers, and through DecodePlan on a
+    2-stripe slab (the batched launch shape the bench times)."""
+    import torch
+    g = golden["c4_full_inconsistent"]
+    k, m, size = g["k"], g["m"], g["size"]
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    for case in g["cases"]:
+        er, rko = case["erasures"], case["row_k_ones"]
+        if path == "sync-device":
+            bufs = to_dev(c4_inputs, gpu)
+            rc = ec.jerasure.jerasure_matrix_decode(k, m, 8, M, rko, er, bufs[:k], bufs[k:], size)
+            got = [digests(to_host(bufs), size)]
+        elif path == "sync-host":
+            bufs = [b.copy() for b in c4_inputs]
+            rc = ec.jerasure.jerasure_matrix_decode(k, m, 8, M, rko, er, bufs[:k], bufs[k:], size)
+            got = [digests(bufs, size)]
+        else:
+            slab, shards = ec.alloc_stripes(2, k, m, size)
+            for st in shards:
+                for i in range(k + m):
+                    st[i].copy_(torch.from_numpy(np.ascontiguousarray(c4_inputs[i][:size])))
+            ec.DecodePlan(k, m, M, er, rko).bind_stripes(shards, size).launch()
+            torch.cuda.synchronize()
+            rc = 0
+            got = [[fnv1a64(t.cpu().numpy()) for t in st] for st in shards]
+        assert rc == case["rc"], (path, er, rko)
+        for d in got:
+            assert d == case["digests"], (path, er, rko)
+
+
 def test_dotprod_golden(ec, gpu, golden):
     for t, case in enumerate(golden["dotprod"]):
         k, m, size = case["k"], case["m"], case["size"]

@@ -102,6 +102,21 @@ def test_decode_inconsistent_inputs(restatement, golden):
         assert [fnv1a64(x[:size]) for x in data + coding] == case["digests"], (case["erasures"], case["row_k_ones"])
 
 
+def test_decode_inconsistent_full_size_c4(restatement, golden):
+    """BASELINE config 4 at 4 MiB on inputs that are not a codeword: the
+    restatement's survivor choice and re-encode against the reference's
+    digests (golden["c4_full_inconsistent"])."""
+    g = golden["c4_full_inconsistent"]
+    k, m, size = g["k"], g["m"], g["size"]
+    M = restatement.vandermonde_coding_matrix(k, m)
+    for case in g["cases"]:
+        data = shards(g["cfg"], 7, k, size)
+        coding = shards(g["cfg"], 7, m, size, first=k)
+        rc = restatement.matrix_decode(k, m, M, case["row_k_ones"], case["erasures"], data, coding, size)
+        assert rc == case["rc"]
+        assert [fnv1a64(x[:size]) for x in data + coding] == case["digests"], (case["erasures"], case["row_k_ones"])
+
+
 def test_dotprod_cases(restatement, golden):
     for t, case in enumerate(golden["dotprod"]):
         k, m, size = case["k"], case["m"], case["size"]

@@ -4,8 +4,9 @@ tables and stats; the replacement must not).
 tests/sanitize/host_harness.cpp drives the host-only part of libecgpu --
 field tables, matrix construction and inversion, the fused decode planner
 over every RS(10,4) pattern of up to 5 erasures, bit-matrix / schedule
-construction, the CPU fallback's executor (against the reference's
-sequential semantics, aliasing included) and its bookkeeping -- built from
+construction, the CPU executor at every SIMD level the host has (against
+the reference's sequential semantics, aliasing and > 4 output rows included)
+and its bookkeeping -- built from
 csrc/ with g++:
 
 * AddressSanitizer + UndefinedBehaviorSanitizer (+ LeakSanitizer), one thread;
@@ -33,7 +34,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "erasure_coding_test_amd", "csrc")
 HOST_SRCS = ["gf_host.cpp", "matrix_host.cpp", "planner.cpp", "schedule_host.cpp", "capi_host.cpp", "contract_host.cpp",
-             "knobs.cpp", "cpu_fallback.cpp"]
+             "knobs.cpp", "cpu_fallback.cpp", "cpu_exec.cpp"]
 HARNESS = os.path.join(ROOT, "tests", "sanitize", "host_harness.cpp")
 PIPE_HARNESS = os.path.join(ROOT, "tests", "sanitize", "pipeline_harness.cpp")
 TSAN_ENV = {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}

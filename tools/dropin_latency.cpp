@@ -35,11 +35,28 @@
 #include "reed_sol.h"
 
 // libecgpu.so (include/ecgpu.h): no timed call may have completed on the CPU
-// fallback; the tool turns it off and reports the count.
+// fallback; the tool turns it off and reports the count.  Every
+// case runs twice: mode "gpu" (ECGPU_MIN_OFFLOAD_KIB=0, every call on the
+// MI355X) and mode "lib" (the library's defaults: calls below the measured
+// crossover on its CPU executor, counted in "cpu_calls").
 extern "C" long ecgpu_fallback_count(void);
+extern "C" long ecgpu_cpu_call_count(void);
 extern "C" int ecgpu_set_knob(const char* name, int value);
+extern "C" int ecgpu_reset_knob(const char* name);
 
 namespace {
+
+const char* g_mode = "lib";
+
+// "mode" and this case's CPU-executor calls, spliced before a line's closing brace
+long g_cpu0 = 0;
+void begin_case() { g_cpu0 = ecgpu_cpu_call_count(); }
+void end_line(const char* json) {
+  std::string s(json);
+  while (!s.empty() && (s.back() == '\n' || s.back() == '}')) s.pop_back();
+  std::printf("%s, \"mode\": \"%s\", \"cpu_calls\": %ld}\n", s.c_str(), g_mode, ecgpu_cpu_call_count() - g_cpu0);
+  std::fflush(stdout);
+}
 
 double now_us() {
   using namespace std::chrono;
@@ -61,6 +78,7 @@ struct Case {
 };
 
 void client_case(const Case& c, bool stripe_buffer, const int* erased, int n_erased) {
+  begin_case();
   int* matrix = reed_sol_vandermonde_coding_matrix(c.k, c.m, 8);
   std::vector<char*> data(size_t(c.k)), coding(size_t(c.m));
   char* buffer = stripe_buffer ? static_cast<char*>(std::malloc(size_t(c.k) * size_t(c.size))) : nullptr;
@@ -94,14 +112,15 @@ void client_case(const Case& c, bool stripe_buffer, const int* erased, int n_era
   }
   const double e = median(enc), d = median(dec);
   std::string er;
+  char line[1024];
   for (int i = 0; i < n_erased; ++i) er += (i ? "," : "") + std::to_string(erased[i]);
-  std::printf(
+  std::snprintf(line, sizeof line,
       "{\"case\": \"%s\", \"buffers\": \"%s\", \"encode_us\": %.1f, \"decode_us\": %.1f, \"erasures\": [%s], "
       "\"encode_data_GiBps\": %.2f, \"decode_data_GiBps\": %.2f, \"decode_ok\": %s}\n",
       c.name, buffer ? "client stripe buffer + malloc'd coding (pageable)" : "one malloc per shard (pageable)", e, d,
       er.c_str(), double(c.k) * c.size / (e * 1e-6) / double(1 << 30), double(c.k) * c.size / (d * 1e-6) / double(1 << 30),
       ok ? "true" : "false");
-  std::fflush(stdout);
+  end_line(line);
   if (buffer)
     std::free(buffer);
   else
@@ -112,6 +131,7 @@ void client_case(const Case& c, bool stripe_buffer, const int* erased, int n_era
 
 // Every call decodes a pattern the previous 209 calls did not use.
 void new_pattern_case(int size) {
+  begin_case();
   const int k = 10, m = 4;
   int* matrix = reed_sol_vandermonde_coding_matrix(k, m, 8);
   std::vector<char*> data(static_cast<size_t>(k)), coding(static_cast<size_t>(m));
@@ -141,11 +161,12 @@ void new_pattern_case(int size) {
         ok = ok && std::memcmp(data[size_t(p[size_t(i)])], orig[size_t(p[size_t(i)])].data(), size_t(size)) == 0;
       if (pass == 1) t.push_back(t1 - t0);
     }
-  std::printf(
+  char line[1024];
+  std::snprintf(line, sizeof line,
       "{\"case\": \"C4 new erasure pattern per call\", \"workload\": \"RS(10,4) decode, %d-byte pageable shards, "
       "cycling through all %zu 4-of-10 data patterns\", \"decode_us\": %.1f, \"decode_ok\": %s}\n",
       size, patterns.size(), median(t), ok ? "true" : "false");
-  std::fflush(stdout);
+  end_line(line);
   for (auto* p : data) std::free(p);
   for (auto* p : coding) std::free(p);
   std::free(matrix);
@@ -153,6 +174,7 @@ void new_pattern_case(int size) {
 
 // ecx_datanode_main.cpp:699-735, unchanged, one arriving block at a time.
 void ecx_case(int k, int m, int block_size, int stripes) {
+  begin_case();
   int* matrix = reed_sol_vandermonde_coding_matrix(k, m, 8);
   char* block_multiply_m = static_cast<char*>(std::malloc((size_t(block_size) + sizeof(long)) * size_t(m)));
   std::vector<char*> blocks(static_cast<size_t>(k));
@@ -196,12 +218,13 @@ void ecx_case(int k, int m, int block_size, int stripes) {
     ok = ok && std::memcmp(coding[size_t(i)], block_multiply_m + size_t(i) * (size_t(block_size) + sizeof(long)),
                            size_t(block_size)) == 0;
   const double b = median(per_block);
-  std::printf(
+  char line[1024];
+  std::snprintf(line, sizeof line,
       "{\"case\": \"ECX per-block sequence RS(%d,%d)\", \"workload\": \"ecx_datanode_main.cpp:699-735 unchanged, "
       "%d-byte blocks, m separate galois_* calls per block (pageable)\", \"per_block_us\": %.1f, "
       "\"block_GiBps\": %.3f, \"parity_ok\": %s}\n",
       k, m, block_size, b, double(block_size) / (b * 1e-6) / double(1 << 30), ok ? "true" : "false");
-  std::fflush(stdout);
+  end_line(line);
   for (auto* p : coding) std::free(p);
   for (auto* p : blocks) std::free(p);
   std::free(block_multiply_m);
@@ -279,11 +302,16 @@ int main(int argc, char** argv) {
       if (std::strncmp(c.name, only, std::strlen(only)) == 0) client_case(c, true, e0, 1);
     return report_fallbacks();
   }
-  for (int stripe_buffer = 1; stripe_buffer >= 0; --stripe_buffer)
-    for (const Case& c : cases) client_case(c, stripe_buffer != 0, e0, 1);
-  client_case({"C4 RS(10,4) 4 MiB", 10, 4, 4 << 20, 30}, true, e0123, 4);
-  new_pattern_case(4096);
-  ecx_case(3, 3, 349525, quick ? 10 : 40);
-  ecx_case(10, 4, 349525, quick ? 4 : 12);
+  for (const char* mode : {"gpu", "lib"}) {
+    g_mode = mode;
+    ecgpu_reset_knob("ECGPU_MIN_OFFLOAD_KIB");
+    if (std::strcmp(mode, "gpu") == 0) ecgpu_set_knob("ECGPU_MIN_OFFLOAD_KIB", 0);
+    for (int stripe_buffer = 1; stripe_buffer >= 0; --stripe_buffer)
+      for (const Case& c : cases) client_case(c, stripe_buffer != 0, e0, 1);
+    client_case({"C4 RS(10,4) 4 MiB", 10, 4, 4 << 20, 30}, true, e0123, 4);
+    new_pattern_case(4096);
+    ecx_case(3, 3, 349525, quick ? 10 : 40);
+    ecx_case(10, 4, 349525, quick ? 4 : 12);
+  }
   return report_fallbacks();
 }

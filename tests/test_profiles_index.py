@@ -25,6 +25,69 @@ def test_bench_traffic_record_is_committed():
         assert json.load(open(os.path.join(PROF, f)))["kernel_build_id"] == summary["kernel_build_id"]
 
 
+def _latest_rocprof_summary():
+    import re
+    names = sorted(f for f in os.listdir(PROF) if re.fullmatch(r"r\d\d_rocprof_summary\.json", f))
+    return names[-1], json.load(open(os.path.join(PROF, names[-1])))
+
+
+def _ranges(cell):
+    """'0.889–0.898 ms' -> [(0.889, 0.898)]; 'a–b / c' -> [(a, b), (c, c)]."""
+    import re
+    out = []
+    for part in cell.replace("ms", "").split("/"):
+        nums = [float(x) for x in re.findall(r"\d+\.\d+", part)]
+        assert nums, cell
+        out.append((min(nums), max(nums)))
+    return out
+
+
+def test_kernel_bound_table_brackets_the_latest_rocprof_medians():
+    """DESIGN §5's bound table (time and fraction of the
+    8 TB/s spec per BASELINE launch) must bracket the medians of the latest
+    committed rocprof summary, so a stale row fails here."""
+    name, summary = _latest_rocprof_summary()
+    k = summary["kernels"]
+    design = open(os.path.join(ROOT, "DESIGN.md")).read()
+    section = design[design.index("**What bounds each kernel**"):design.index("### 5.1")]
+    rows = {}
+    for line in section.splitlines():
+        cells = [c.strip() for c in line.strip().strip("|").split("|")]
+        if len(cells) == 5 and cells[0].startswith("`gf_apply<"):
+            rows[cells[0]] = cells
+    want = {  # table row -> summary kernels, in the row's "a / b" order
+        "`gf_apply<10,4,3>`": ["encode"],
+        "`gf_apply<10,1,4>`": ["decode"],
+        "`gf_apply<10,1,1>`": ["C3_decode_parity"],
+        "`gf_apply<10,4,0>`": ["C4_decode_0123"],
+        "`gf_apply<6,3,3>` / `<12,4,3>`": ["C2_encode", "C5_encode"],
+    }
+    tol = 0.0015  # the table rounds to three decimals
+    for row, keys in want.items():
+        assert row in rows, (row, sorted(rows))
+        _, _, t_cell, f_cell, _ = rows[row]
+        times, fracs = _ranges(t_cell), _ranges(f_cell)
+        assert len(times) == len(fracs) == len(keys), (row, t_cell, f_cell)
+        for key, (t_lo, t_hi), (f_lo, f_hi) in zip(keys, times, fracs):
+            med_ns = k[key]["median_duration_ns"]
+            frac = k[key]["algorithmic_bytes_per_launch"] / med_ns / 8000.0
+            assert t_lo - tol <= med_ns / 1e6 <= t_hi + tol, (name, row, key, med_ns, t_cell)
+            assert f_lo - tol <= frac <= f_hi + tol, (name, row, key, round(frac, 4), f_cell)
+
+
+def test_design_test_count_matches_the_latest_gpu_record():
+    """the `-m gpu` test count DESIGN §3 states is the
+    latest committed GPU-suite record's."""
+    import re
+    recs = sorted(f for f in os.listdir(PROF) if re.fullmatch(r"r\d\d_gputest\.txt", f))
+    if not recs:
+        return
+    passed = re.findall(r"(\d+) passed", open(os.path.join(PROF, recs[-1])).read())
+    design = open(os.path.join(ROOT, "DESIGN.md")).read()
+    stated = re.search(r"`-m gpu`, (\d+) tests", design).group(1)
+    assert passed and stated == passed[-1], (recs[-1], passed, stated)
+
+
 def _skew_table():
     """{size: skew} from csrc/shard_stride.hpp's kSkewTable."""
     import re

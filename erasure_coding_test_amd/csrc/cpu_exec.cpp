@@ -24,8 +24,9 @@ namespace {
 constexpr int kRows = 4;
 
 // Bytes of every buffer per step where outputs go through temporaries (more
-// than kRows rows with an output that is also a source; the non-GFNI paths
-// always): every source block is read before any output block is written.
+// than kRows rows with an output that is also a source; the per-term paths --
+// w = 16 / 32 without GFNI, scalar -- always): every source block is read
+// before any output block is written.
 // 32 KiB: 14 RS(10,4) buffers stay in a core's L2.  A multiple of 64.
 constexpr int64_t kChunk = int64_t(32) << 10;
 
@@ -36,6 +37,21 @@ int detected_level() {
     return __builtin_cpu_supports("avx2") ? 1 : 0;
   }();
   return level;
+}
+
+// GF(2^8): c*x = lo[x & 15] ^ hi[x >> 4] (the north star's nibble split)
+struct Nib8 {
+  uint8_t lo[16], hi[16];
+};
+
+Nib8 nib8(uint32_t c) {
+  Nib8 t;
+  const auto& T = gf8().mul[c & 0xFFu];
+  for (int v = 0; v < 16; ++v) {
+    t.lo[v] = T[v];
+    t.hi[v] = T[v << 4];
+  }
+  return t;
 }
 
 // ================================================ AVX-512 + GFNI ====
@@ -151,15 +167,65 @@ GroupFn gfni_group(int R, int w) {
   return (w == 8 ? t8 : w == 16 ? t16 : t32)[R - 1];
 }
 
+// ====================================== AVX2 / scalar (no GFNI) ====
+void mul_add8_scalar(uint8_t* acc, const uint8_t* src, int64_t n, const Nib8& t) {
+  for (int64_t i = 0; i < n; ++i) acc[i] ^= uint8_t(t.lo[src[i] & 15] ^ t.hi[src[i] >> 4]);
+}
+
+// R <= kRows rows of a w = 8 map on AVX2, gfni8_group's shape: per 32-byte
+// column every source is loaded and split into nibbles once, R accumulators
+// stay in registers, one store per row.  T[j * R + r] are coefficient (r, j)'s
+// nibble tables (c = 1 and c = 0 are ordinary tables: identity and zero).
+template <int R>
+ECGPU_TARGET_AVX2 void avx2_group8(const uint8_t* const* src, int K, uint8_t* const* dst, const Nib8* T, int64_t n) {
+  const __m256i low4 = _mm256_set1_epi8(0x0f);
+  int64_t i = 0;
+  for (; i + 32 <= n; i += 32) {
+    __m256i acc[R];
+#pragma GCC unroll 4
+    for (int r = 0; r < R; ++r) acc[r] = _mm256_setzero_si256();
+    for (int j = 0; j < K; ++j) {
+      const __m256i x = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src[j] + i));
+      const __m256i l = _mm256_and_si256(x, low4);
+      const __m256i h = _mm256_and_si256(_mm256_srli_epi64(x, 4), low4);
+      const Nib8* t = T + size_t(j) * R;
+#pragma GCC unroll 4
+      for (int r = 0; r < R; ++r) {
+        const __m256i tlo = _mm256_broadcastsi128_si256(_mm_loadu_si128(reinterpret_cast<const __m128i*>(t[r].lo)));
+        const __m256i thi = _mm256_broadcastsi128_si256(_mm_loadu_si128(reinterpret_cast<const __m128i*>(t[r].hi)));
+        acc[r] = _mm256_xor_si256(acc[r], _mm256_xor_si256(_mm256_shuffle_epi8(tlo, l), _mm256_shuffle_epi8(thi, h)));
+      }
+    }
+#pragma GCC unroll 4
+    for (int r = 0; r < R; ++r) _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst[r] + i), acc[r]);
+  }
+  for (; i < n; ++i) {  // the last < 32 bytes: every row's byte before any store (an output may be a source)
+    uint8_t a[R] = {};
+    for (int j = 0; j < K; ++j) {
+      const uint8_t x = src[j][i];
+      for (int r = 0; r < R; ++r) {
+        const Nib8& t = T[size_t(j) * R + size_t(r)];
+        a[r] ^= uint8_t(t.lo[x & 15] ^ t.hi[x >> 4]);
+      }
+    }
+    for (int r = 0; r < R; ++r) dst[r][i] = a[r];
+  }
+}
+
+using Avx2GroupFn = void (*)(const uint8_t* const*, int, uint8_t* const*, const Nib8*, int64_t);
+
+// ================================= row groups (GFNI; AVX2 at w = 8) ====
 // One group's sources (those with a non-zero coefficient in its rows) and
-// their matrices in gfni*_group's layout.
+// their coefficients in gfni*_group's (A) or avx2_group8's (T) layout.
 struct Group {
   int r0 = 0, R = 0;
   std::vector<int> js;
   std::vector<uint64_t> A;
+  std::vector<Nib8> T;
 };
 
-std::vector<Group> plan_groups(const FusedOp& op) {
+// level 2: affine matrices; level 1 (w = 8 only): nibble tables.
+std::vector<Group> plan_groups(const FusedOp& op, int level) {
   const int rows = int(op.dsts.size()), nsrc = int(op.srcs.size()), B = op.w / 8;
   const uint32_t mask = op.w == 32 ? 0xFFFFFFFFu : (uint32_t(1) << op.w) - 1u;
   std::vector<Group> groups;
@@ -174,6 +240,10 @@ std::vector<Group> plan_groups(const FusedOp& op) {
       g.js.push_back(j);
       for (int r = 0; r < g.R; ++r) {
         const uint32_t c = op.coef[size_t(r0 + r) * nsrc + j] & mask;
+        if (level < 2) {
+          g.T.push_back(nib8(c));
+          continue;
+        }
         for (int s = 0; s < B; ++s)
           for (int a = 0; a < B; ++a) g.A.push_back(gf_affine_block(c, op.w, a, (a + s) % B));
       }
@@ -185,25 +255,29 @@ std::vector<Group> plan_groups(const FusedOp& op) {
 
 // Runs `g` over [off, off + n) of the sources into `dst` (R pointers, already
 // offset).
-void run_group(const FusedOp& op, const Group& g, int64_t off, uint8_t* const* dst, int64_t n) {
+void run_group(const FusedOp& op, const Group& g, int64_t off, uint8_t* const* dst, int64_t n, int level) {
   if (g.js.empty()) {
     for (int r = 0; r < g.R; ++r) std::memset(dst[r], 0, size_t(n));
     return;
   }
   std::vector<const uint8_t*> src(g.js.size());
   for (size_t i = 0; i < g.js.size(); ++i) src[i] = static_cast<const uint8_t*>(op.srcs[size_t(g.js[i])]) + off;
-  gfni_group(g.R, op.w)(src.data(), int(src.size()), dst, g.A.data(), n);
+  if (level >= 2) return gfni_group(g.R, op.w)(src.data(), int(src.size()), dst, g.A.data(), n);
+  static const Avx2GroupFn t8[kRows] = {avx2_group8<1>, avx2_group8<2>, avx2_group8<3>, avx2_group8<4>};
+  t8[g.R - 1](src.data(), int(src.size()), dst, g.T.data(), n);
 }
 
-void apply_gfni(const FusedOp& op, int64_t size) {
+// Row groups of <= kRows outputs, each one pass over its sources (level 2:
+// any w; level 1: w = 8).
+void apply_groups(const FusedOp& op, int64_t size, int level) {
   const int rows = int(op.dsts.size());
-  const std::vector<Group> groups = plan_groups(op);
+  const std::vector<Group> groups = plan_groups(op, level);
   if (!(op.dst_is_src && rows > kRows)) {
     // direct: a group's outputs are read by no later group
     for (const Group& g : groups) {
       uint8_t* dst[kRows];
       for (int r = 0; r < g.R; ++r) dst[r] = static_cast<uint8_t*>(op.dsts[size_t(g.r0 + r)]);
-      run_group(op, g, 0, dst, size);
+      run_group(op, g, 0, dst, size, level);
     }
     return;
   }
@@ -214,49 +288,11 @@ void apply_gfni(const FusedOp& op, int64_t size) {
     for (const Group& g : groups) {
       uint8_t* dst[kRows];
       for (int r = 0; r < g.R; ++r) dst[r] = tmp.data() + size_t(g.r0 + r) * size_t(chunk);
-      run_group(op, g, a, dst, n);
+      run_group(op, g, a, dst, n, level);
     }
     for (int r = 0; r < rows; ++r)
       std::memcpy(static_cast<uint8_t*>(op.dsts[size_t(r)]) + a, tmp.data() + size_t(r) * size_t(chunk), size_t(n));
   }
-}
-
-// ====================================== AVX2 / scalar (no GFNI) ====
-// GF(2^8): c*x = lo[x & 15] ^ hi[x >> 4] (the north star's nibble split)
-struct Nib8 {
-  uint8_t lo[16], hi[16];
-};
-
-Nib8 nib8(uint32_t c) {
-  Nib8 t;
-  const auto& T = gf8().mul[c & 0xFFu];
-  for (int v = 0; v < 16; ++v) {
-    t.lo[v] = T[v];
-    t.hi[v] = T[v << 4];
-  }
-  return t;
-}
-
-void mul_add8_scalar(uint8_t* acc, const uint8_t* src, int64_t n, const Nib8& t) {
-  for (int64_t i = 0; i < n; ++i) acc[i] ^= uint8_t(t.lo[src[i] & 15] ^ t.hi[src[i] >> 4]);
-}
-
-// 32 bytes per step: two vpshufb lookups (16-entry tables in each 128-bit
-// lane) and the XORs.
-ECGPU_TARGET_AVX2 void mul_add8_avx2(uint8_t* acc, const uint8_t* src, int64_t n, const Nib8& t) {
-  const __m256i tlo = _mm256_broadcastsi128_si256(_mm_loadu_si128(reinterpret_cast<const __m128i*>(t.lo)));
-  const __m256i thi = _mm256_broadcastsi128_si256(_mm_loadu_si128(reinterpret_cast<const __m128i*>(t.hi)));
-  const __m256i low4 = _mm256_set1_epi8(0x0f);
-  int64_t i = 0;
-  for (; i + 32 <= n; i += 32) {
-    const __m256i x = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
-    const __m256i l = _mm256_and_si256(x, low4);
-    const __m256i h = _mm256_and_si256(_mm256_srli_epi64(x, 4), low4);
-    const __m256i p = _mm256_xor_si256(_mm256_shuffle_epi8(tlo, l), _mm256_shuffle_epi8(thi, h));
-    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(acc + i));
-    _mm256_storeu_si256(reinterpret_cast<__m256i*>(acc + i), _mm256_xor_si256(a, p));
-  }
-  mul_add8_scalar(acc + i, src + i, n - i, t);
 }
 
 // GF(2^16) / GF(2^32) words: c*x = XOR_t T_t[nibble t of x]
@@ -327,7 +363,7 @@ struct Term {
 void apply_term(uint8_t* acc, const uint8_t* src, int64_t n, const Term& t, int w, int level) {
   if (t.c == 0) return;
   if (t.c == 1) return xor_into(acc, src, n, level);
-  if (w == 8) return level >= 1 ? mul_add8_avx2(acc, src, n, t.t8) : mul_add8_scalar(acc, src, n, t.t8);
+  if (w == 8) return mul_add8_scalar(acc, src, n, t.t8);  // level 0 (levels 1-2 take apply_groups)
   if (w == 16) return mul_addw<uint16_t>(acc, src, n, t.t16);
   mul_addw<uint32_t>(acc, src, n, t.t32);
 }
@@ -387,7 +423,7 @@ void cpu_apply(const FusedOp& op, int64_t size) { cpu_apply(op, size, cpu_simd_l
 void cpu_apply(const FusedOp& op, int64_t size, int level) {
   if (op.dsts.empty() || size <= 0) return;
   level = std::max(0, std::min(level, detected_level()));
-  if (level >= 2) return apply_gfni(op, size);
+  if (level >= 2 || (level == 1 && op.w == 8)) return apply_groups(op, size, level);
   apply_nibbles(op, size, level);
 }
 

@@ -13,7 +13,8 @@
 // (any field polynomial: the matrix is built from the reference's own
 // products, gf_host).  w = 16 / 32 words are B x B blocks of such matrices
 // over byte rotations of the word.  Without GFNI: w = 8 by the north star's
-// nibble split on AVX2 (two vpshufb per 32 bytes), then scalar.
+// nibble split on AVX2 (two vpshufb per 32 bytes, rows grouped like the
+// GFNI path: each source loaded once per 32-byte column), then scalar.
 //
 // Semantics: dst[r] = XOR_j coef[r][j] * src[j]; every byte column is
 // independent and every source column is read before any output column is

@@ -3,7 +3,8 @@
 # copies and the pipelines with one process, then two processes on cuda:0
 # (each timed pass barrier-started), then the same two-process encode and
 # duplex legs under rocprofv3 --kernel-trace --memory-copy-trace (one process
-# each, no counters), summarised by tools/copy_overlap.py.
+# each, no counters), summarised by tools/copy_overlap.py;
+# then the default bench line.
 set -e
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
@@ -46,4 +47,6 @@ timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format c
     python3 -u tools/e2e_pair.py --world 1 --port 29631 --legs pipe_encode,duplex --passes 2 --tag prof_one \
     > $O/prof_one.jsonl 2> $O/prof_one.err
 python3 tools/copy_overlap.py $P/r0 > $O/overlap_one.json
+# the default bench line on this tree (w = 8 kernel build unchanged: no new profile pass)
+timeout -k 10 400 python3 -u bench.py > $O/bench.json 2> $O/bench.err
 echo session_ok

@@ -1072,12 +1072,14 @@ def main(argv=None):
                            for name, e in configs.items()}
     if e2e_mine is not None:
         mine["e2e"] = e2e_mine
-    # no GPU result may come from the drop-in's CPU fallback; the
-    # package keeps it off, and a nonzero count fails the run
+    # no GPU result may come from the drop-in's CPU fallback or
+    # its CPU executor for small host calls (ECGPU_MIN_OFFLOAD_KIB); the
+    # package keeps both off, and a nonzero count fails the run
     mine["cpu_fallbacks"] = N.fallback_count()
+    mine["cpu_calls"] = N.cpu_call_count()
     per_rank = gather(mine, world)
     ok = (all(p["parity_ok"] for p in per_rank) and (c5 is None or c5["parity_ok"]) and
-          all(p["cpu_fallbacks"] == 0 for p in per_rank))
+          all(p["cpu_fallbacks"] == 0 and p["cpu_calls"] == 0 for p in per_rank))
     devices_ok, devices_note = distinct_devices(per_rank, rehearsal)
     barrier(world)  # every rank's GPU work is done: the CPU baseline below runs alone
 
@@ -1165,6 +1167,7 @@ def main(argv=None):
             "e2e": e2e,
             **({"e2e_per_rank": e2e_per_rank, "e2e_aggregate": e2e_agg} if world > 1 else {}),
             "cpu_fallbacks": sum(p["cpu_fallbacks"] for p in per_rank),
+            "cpu_calls": sum(p["cpu_calls"] for p in per_rank),
             "selfcheck_parity_ok": ok,
             "selfcheck_vs_reference_cpu": cpu_ok,
             "e2e_ok": e2e_ok,

@@ -57,6 +57,7 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_GPU", "gpu", 1},
     {"ECGPU_MIN_OFFLOAD_KIB", "min_offload_kib", 1024},
     {"ECGPU_CPU_SIMD", "cpu_simd", -1},
+    {"ECGPU_PIPE_ZC", "pipe_zc", 0},
 };
 
 constexpr int kUnset = INT_MIN;

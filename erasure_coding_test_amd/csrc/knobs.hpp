@@ -51,6 +51,9 @@ enum class Knob : int {
                     // buffers x size) runs on the CPU executor; 0 = every call on the GPU
   kCpuSimd,         // ECGPU_CPU_SIMD: the CPU executor's SIMD level, -1 the host's best, 2 AVX-512 + GFNI,
                     // 1 AVX2, 0 scalar (never above what the host has)
+  kPipeZc,          // ECGPU_PIPE_ZC: host pipelines over pinned host shards -- 0 DMA in and out, 1 DMA in and
+                    // the kernel writes the outputs into the pinned host buffers, 2 the kernel reads the
+                    // sources and writes the outputs in host memory (no DMA); read at pipeline creation
   kCount
 };
 

@@ -44,6 +44,12 @@ struct PipeDevice {
   std::vector<ecgpu_plan*> plans;     // one bound plan per ring slot (none when nsrc or rows is 0)
   hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
   std::vector<hipEvent_t> loaded, computed, drained;
+  // ECGPU_PIPE_ZC (read at creation): 1 the kernel writes the outputs into
+  // pinned host buffers in place, 2 it also reads the sources there (no DMA);
+  // a stripe whose buffers are not all mapped host memory takes the DMA path.
+  int zc_mode = 0;
+  FusedOp zc_op;                      // the map for gf_apply_inl launches (coef only; pointers per stripe)
+  std::vector<char> zc_slot;          // per slot: its outputs were written in place (no D2H)
 
   int nsrc() const { return int(src_ids.size()); }
   int rows() const { return int(out_ids.size()); }
@@ -51,11 +57,56 @@ struct PipeDevice {
     return d_ring + slot_stride * (size_t(nsrc() + rows()) * size_t(slot) + size_t(j));
   }
 
+  // The stripe's zero-copy launch (ECGPU_PIPE_ZC), or false when a buffer is
+  // not mapped host memory: sources from the slot after its H2D (mode 1) or
+  // read in place (mode 2), outputs written in place over PCIe.
+  int stage_zc(int sl, const std::function<char*(int)>& host, bool* done) {
+    *done = false;
+    const int ns = nsrc(), nr = rows();
+    const size_t bytes = size_t(size);
+    std::vector<uint8_t*> dp(size_t(nr), nullptr);
+    std::vector<const uint8_t*> sp(size_t(ns), nullptr);
+    for (int i = 0; i < nr; ++i) {
+      void* dv = nullptr;
+      if (!host_mapped(host(out_ids[i]), bytes, &dv)) return ECGPU_OK;
+      dp[size_t(i)] = static_cast<uint8_t*>(dv);
+    }
+    for (int j = 0; j < ns; ++j) {
+      void* dv = nullptr;
+      if (zc_mode == 2 && !host_mapped(host(src_ids[j]), bytes, &dv)) return ECGPU_OK;
+      sp[size_t(j)] = zc_mode == 2 ? static_cast<const uint8_t*>(dv) : slot_shard(sl, j);
+    }
+    if (zc_mode == 1) {
+      std::vector<char*> hp;
+      for (int j = 0; j < ns; ++j) hp.push_back(host(src_ids[j]));
+      if (int rc = copy_shards(true, slot_shard(sl, 0), slot_stride, hp, bytes, s_h2d)) return rc;
+    }
+    ECGPU_HIP(hipEventRecord(loaded[sl], s_h2d));
+    ECGPU_HIP(hipStreamWaitEvent(s_comp, loaded[sl], 0));
+    // the host outputs of the stripe that last used this slot were written by
+    // an earlier launch on this same stream: no event needed between them
+    if (int rc = launch_inline(zc_op, sp, dp, size, s_comp, /*host_io=*/true)) return rc;
+    ECGPU_HIP(hipEventRecord(computed[sl], s_comp));
+    *done = true;
+    return ECGPU_OK;
+  }
+
   // H2D of the sources (s_h2d), the fused apply (s_comp), the computed event.
   int stage(int sl, char** data_ptrs, char** coding_ptrs, std::vector<char*>* out, bool* out_blocks) {
     auto host = [&](int id) { return id < k ? data_ptrs[id] : coding_ptrs[id - k]; };
     const int ns = nsrc(), nr = rows();
     const size_t bytes = size_t(size);
+    zc_slot[size_t(sl)] = 0;
+    if (zc_mode != 0 && ns > 0 && nr > 0) {
+      bool done = false;
+      if (int rc = stage_zc(sl, host, &done)) return rc;
+      if (done) {
+        zc_slot[size_t(sl)] = 1;
+        out->clear();
+        *out_blocks = false;
+        return ECGPU_OK;
+      }
+    }
     if (nr > 0) {  // nothing to read when no shard is written
       std::vector<char*> hp;
       for (int j = 0; j < ns; ++j) hp.push_back(host(src_ids[j]));
@@ -83,7 +134,8 @@ struct PipeDevice {
   // D2H of a slot's outputs (s_d2h, after the slot's compute), then drained.
   int d2h(int sl, const std::vector<char*>& hp) {
     ECGPU_HIP(hipStreamWaitEvent(s_d2h, computed[sl], 0));
-    if (int rc = copy_shards(false, slot_shard(sl, nsrc()), slot_stride, hp, size_t(size), s_d2h)) return rc;
+    if (!zc_slot[size_t(sl)])  // (written in place by the kernel: nothing to copy)
+      if (int rc = copy_shards(false, slot_shard(sl, nsrc()), slot_stride, hp, size_t(size), s_d2h)) return rc;
     ECGPU_HIP(hipEventRecord(drained[sl], s_d2h));
     return ECGPU_OK;
   }
@@ -159,6 +211,13 @@ ecgpu_pipeline* pipeline_build(int k, int m, int rows, int nsrc, const int* coef
     for (auto& ev : *v)
       if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "event");
   }
+  d.zc_slot.assign(size_t(depth), 0);
+  d.zc_op.w = 8;
+  d.zc_op.coef.assign(coef, coef + size_t(rows) * size_t(nsrc));
+  d.zc_op.srcs.assign(size_t(nsrc), nullptr);  // counts only (inline_ok); pointers are per stripe
+  d.zc_op.dsts.assign(size_t(rows), nullptr);
+  d.zc_mode = std::max(0, std::min(2, knob(Knob::kPipeZc)));
+  if (d.zc_mode && !(nsrc > 0 && rows > 0 && inline_ok(d.zc_op, size))) d.zc_mode = 0;
   if (nsrc > 0 && rows > 0) {
     for (int sl = 0; sl < depth; ++sl) {
       std::vector<const uint8_t*> src(static_cast<size_t>(nsrc));

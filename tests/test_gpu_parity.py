@@ -812,6 +812,75 @@ def test_sync_calls_on_host_stripe_slab(ec, gpu, restatement, size, pinned, pitc
     assert not slab[:, size:].any() and not slab[k + 2:].any()
 
 
+@pytest.mark.parametrize("zc", [1, 2])
+@pytest.mark.parametrize("memory", ["slab_pinned", "shards_pinned", "registered", "pageable", "mixed"])
+@pytest.mark.parametrize("size", [(1 << 20) + 3, 4 << 20])
+def test_host_pipeline_zero_copy_modes(ec, gpu, restatement, knobs, zc, memory, size):
+    """ECGPU_PIPE_ZC (round 6): 1 -- sources by DMA, the kernel writes the
+    outputs into the pinned host buffers in place; 2 -- the kernel also reads
+    the sources in place (no DMA).  A stripe whose buffers are not all mapped
+    host memory (pageable, or a pageable output among pinned ones) takes the
+    DMA path in the same pipeline.  Encode against the oracle, nothing written
+    past a shard, then a decode pipeline (data, data, parity erased) restores
+    every byte."""
+    import torch
+    knobs.set("pipe_zc", zc)
+    k, m, stripes = 10, 4, 5
+    pitch = size + PAD
+    M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    g = torch.Generator().manual_seed(size + zc)
+    if memory == "slab_pinned":
+        slab = torch.full((stripes, k + m, pitch), 0x77, dtype=torch.uint8).pin_memory()
+        bufs = [[slab[s, j] for j in range(k + m)] for s in range(stripes)]
+    else:
+        bufs = [[torch.full((pitch,), 0x77, dtype=torch.uint8) for _ in range(k + m)] for _ in range(stripes)]
+        for s, st in enumerate(bufs):
+            if memory == "shards_pinned" or (memory == "mixed" and s % 2 == 0):
+                bufs[s] = [b.pin_memory() for b in st]
+            elif memory == "mixed":  # pinned sources, one pageable output: the stripe takes the DMA path
+                bufs[s] = [b.pin_memory() for b in st[:k + m - 1]] + [st[-1]]
+    for st in bufs:
+        for j in range(k):
+            st[j][:size] = torch.randint(0, 256, (size,), dtype=torch.uint8, generator=g)
+    if memory == "registered":
+        for st in bufs:
+            for b in st:
+                ec.pipeline.host_register(b.numpy())
+    try:
+        p = ec.HostPipeline(k, m, M, size, depth=3)
+        for st in bufs:
+            p.submit(st[:k], st[k:])
+        p.drain()
+        p.close()
+        want = [[b.clone() for b in st] for st in bufs]
+        for s, st in enumerate(bufs):
+            hd = alloc_shards(k, size, PAD)
+            for j in range(k):
+                hd[j][:size] = st[j][:size].numpy()
+            ref = _encode_ref(restatement, k, m, M, hd, size)
+            for i in range(m):
+                got = st[k + i].numpy()
+                assert np.array_equal(got[:size], ref[i][:size]), (s, i)
+                assert (got[size:] == 0x77).all(), (s, i)
+        er = [1, 6, k + 2]
+        for st in bufs:
+            for e in er:
+                st[e][:size] = 0
+        d = ec.HostPipeline.decoder(k, m, M, er, size, depth=2)
+        for st in bufs:
+            d.submit(st[:k], st[k:])
+        d.drain()
+        d.close()
+        for s in range(stripes):
+            for i in range(k + m):
+                assert torch.equal(bufs[s][i], want[s][i]), (s, i)
+    finally:
+        if memory == "registered":
+            for st in bufs:
+                for b in st:
+                    ec.pipeline.host_unregister(b.numpy())
+
+
 @pytest.mark.parametrize("erasures", [[0], [0, 1, 2, 3], [2, 11], [10, 13], []])
 def test_host_pipeline_decoder_matches_reference_decode(ec, gpu, erasures):
     import torch

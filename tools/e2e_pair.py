@@ -16,6 +16,13 @@ Legs (per rank, `stripes` stripes of pinned host memory [stripes][k+m][S]):
                no compute)
   pipe_encode  ecgpu_pipeline (H2D, encode, D2H overlapped, depth 3)
   pipe_decode  ecgpu_pipeline_create_decode, erasure {0} (10 in, 1 out)
+  pipe_*_zc1   the same with ECGPU_PIPE_ZC=1: the kernel writes the outputs
+               into the pinned host stripes in place (no D2H DMA)
+  pipe_*_zc2   ECGPU_PIPE_ZC=2: the kernel also reads the sources in place
+               (no DMA at all)
+Pipeline legs check the last stripe after the last pass (its outputs zeroed
+before it): encode parity against a device-resident encode, decode against
+the original shard.
 
     python3 tools/e2e_pair.py --rank R --world W --port P [--legs a,b] [--depth 3]
 
@@ -61,6 +68,12 @@ def main():
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     host = torch.empty((n, k + m, S), dtype=torch.uint8).pin_memory()
     host[:, :k].random_(0, 256)
+    for s in range(n):  # valid codewords, so the decode legs have consistent survivors
+        d = host[s, :k].to(dev)
+        par = torch.empty((m, S), dtype=torch.uint8, device=dev)
+        E.encode_plan(k, m, M, 0).bind([[d[j] for j in range(k)]], [[par[i] for i in range(m)]], S).launch()
+        torch.cuda.synchronize(dev)
+        host[s, k:].copy_(par.cpu())
     dk = torch.empty((3, k, S), dtype=torch.uint8, device=dev)
     dm = torch.empty((3, m, S), dtype=torch.uint8, device=dev)
     dm.random_(0, 256)
@@ -94,9 +107,21 @@ def main():
             p.drain()
         return run
 
+    from erasure_coding_test_amd import _native as N
+
+    def pipeline(decode, zc):
+        def make():
+            N.set_knob("pipe_zc", zc)  # read at creation
+            p = (E.HostPipeline.decoder(k, m, M, [0], S, depth=a.depth, device=0) if decode
+                 else E.HostPipeline(k, m, M, S, depth=a.depth, device=0))
+            N.reset_knob("pipe_zc")
+            return p
+        return None, make
+
     legs = {"h2d": (h2d, None), "d2h": (d2h, None), "duplex": (duplex, None),
-            "pipe_encode": (None, lambda: E.HostPipeline(k, m, M, S, depth=a.depth, device=0)),
-            "pipe_decode": (None, lambda: E.HostPipeline.decoder(k, m, M, [0], S, depth=a.depth, device=0))}
+            "pipe_encode": pipeline(False, 0), "pipe_decode": pipeline(True, 0),
+            "pipe_encode_zc1": pipeline(False, 1), "pipe_encode_zc2": pipeline(False, 2),
+            "pipe_decode_zc1": pipeline(True, 1), "pipe_decode_zc2": pipeline(True, 2)}
     for name in a.legs.split(","):
         fn, make = legs[name]
         p = make() if make else None
@@ -104,14 +129,27 @@ def main():
         run()  # warm
         torch.cuda.synchronize(dev)
         ts = []
-        for _ in range(a.passes):
+        ok = None
+        for it in range(a.passes):
+            if p is not None and it == a.passes - 1:
+                # the last pass must rewrite what it outputs: scribble over it first
+                want = host[n - 1].clone()
+                host[:, [0] if name.startswith("pipe_decode") else slice(k, k + m)] = 0
             dist.barrier()
             t0 = time.perf_counter()
             run()
             ts.append(time.perf_counter() - t0)
         if p is not None:
             p.close()
-        mine = {"rank": a.rank, "pass_ms": [round(t * 1e3, 2) for t in ts]}
+            if name.startswith("pipe_encode"):
+                d = host[n - 1, :k].to(dev)
+                ref = torch.empty((m, S), dtype=torch.uint8, device=dev)
+                E.encode_plan(k, m, M, 0).bind([[d[j] for j in range(k)]], [[ref[i] for i in range(m)]], S).launch()
+                torch.cuda.synchronize(dev)
+                ok = bool(torch.equal(ref.cpu(), host[n - 1, k:])) and bool(torch.equal(want, host[n - 1]))
+            else:
+                ok = bool(torch.equal(want, host[n - 1]))
+        mine = {"rank": a.rank, "pass_ms": [round(t * 1e3, 2) for t in ts], "ok": ok}
         allr = [None] * a.world
         dist.all_gather_object(allr, mine)
         if a.rank == 0:
@@ -121,9 +159,9 @@ def main():
                               "unit": "GiB/s (h2d/duplex/pipe: data shards; d2h: parity shards), all ranks",
                               "aggregate_GiBps": [round(x, 2) for x in agg],
                               "aggregate_median_GiBps": round(sorted(agg)[len(agg) // 2], 2),
-                              "per_rank_pass_ms": [r["pass_ms"] for r in allr]}), flush=True)
-    from erasure_coding_test_amd import _native as N
-    assert N.fallback_count() == 0
+                              "per_rank_pass_ms": [r["pass_ms"] for r in allr],
+                              "ok": [r["ok"] for r in allr]}), flush=True)
+    assert N.fallback_count() == 0 and N.cpu_call_count() == 0
     dist.barrier()
     dist.destroy_process_group()
 

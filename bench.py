@@ -683,6 +683,8 @@ def e2e_all_ranks(E, M, k, m, S, erasures, dev, local, world, stripes):
     gpu_node = pci_numa_node(bus)
     before = os.sched_getaffinity(0)
     near = (node_cpus(gpu_node) & before) if gpu_node is not None else set()
+    if os.environ.get("ECGPU_BENCH_E2E_NUMA", "1") == "0":  # A/B switch: leave the affinity alone
+        near = set()
     if near:
         os.sched_setaffinity(0, near)
     try:
@@ -691,6 +693,7 @@ def e2e_all_ranks(E, M, k, m, S, erasures, dev, local, world, stripes):
         os.sched_setaffinity(0, before)
     r["gpu_numa_node"] = gpu_node
     r["threads_on_gpu_node"] = bool(near)
+    r["thread_cpus"] = len(near) if near else len(before)
     return r
 
 

@@ -20,9 +20,10 @@
  * (classified per buffer; host buffers are staged through HBM) and are
  * synchronous: results are valid on return, like the reference.  A call
  * whose buffers are all host memory and that moves fewer than
- * ECGPU_MIN_OFFLOAD_KIB bytes (distinct buffers x size; every such call with
- * ECGPU_GPU=0) runs on the library's own CPU executor, where the GPU round
- * trip would cost more (counted by ecgpu_cpu_call_count).  A HIP failure on
+ * ECGPU_MIN_OFFLOAD_KIB bytes (distinct buffers x size; 16 MiB by default,
+ * the measured crossover of DESIGN.md §8; every such call with ECGPU_GPU=0)
+ * runs on the library's own CPU executor, where the GPU round trip would
+ * cost more (counted by ecgpu_cpu_call_count).  A HIP failure on
  * a call whose buffers are all host memory, before it overwrote one of its
  * sources, completes on the CPU (no new failure modes; counted
  * by ecgpu_fallback_count, the first one logged on stderr) unless the

@@ -309,24 +309,30 @@ def pinned_alias(d, ref, core, run):
     run.check(np.array_equal(buf, want), "pinned in-place region multiply")
 
 
-def fill_hbm(hip):
-    """Allocates device memory until hipMalloc fails (HBM exhausted), so the
-    library's own staging hipMalloc fails for real (SURVEY §8b's contract on
-    a genuine HIP error, not an injected one).  Returns the byte count held."""
+def fill_hbm(hip, leave=16 << 20):
+    """Allocates device memory until less than `leave` bytes are free, so the
+    library's own staging hipMalloc (tens of MiB for a C3 call) fails for real
+    (SURVEY §8b's contract on a genuine HIP error, not an injected one) while
+    the HIP runtime keeps the few MiB its own bookkeeping needs (with HBM
+    exhausted to the last MiB the runtime itself crashed, round 6).  Returns
+    the byte count held and the allocations."""
     hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
     hip.hipMemGetInfo.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
     free, total = ctypes.c_size_t(), ctypes.c_size_t()
-    assert hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) == 0
     held, keep = 0, []
-    chunk = max(free.value - (256 << 20), 1 << 20)
+    chunk = 64 << 30
     while chunk >= (1 << 20):
+        assert hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) == 0
+        if free.value < leave + chunk:
+            chunk //= 2
+            continue
         p = ctypes.c_void_p()
         if hip.hipMalloc(ctypes.byref(p), chunk) == 0:
             keep.append(p)
             held += chunk
         else:
             hip.hipGetLastError()
-            chunk //= 4
+            chunk //= 2
     return held, keep
 
 
@@ -334,10 +340,22 @@ def oom(d, core, golden, run):
     """The client's C3 calls (client_main.cpp:1060, :2118) on one malloc'd
     stripe buffer with HBM full: every staging hipMalloc fails."""
     hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime libecgpu.so is bound to (already loaded)
-    held, keep = fill_hbm(hip)
-    run.held = held
     k, m, size = 10, 4, 4 << 20
     M = matrix(d, k, m)
+    # warm the library first (context, stream, the inline kernels' code
+    # object): the same calls at 64 KiB shards, staged in coherent pinned host
+    # memory (no HBM), on the GPU whatever the small-call threshold
+    core.ecgpu_set_knob.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    core.ecgpu_set_knob(b"ECGPU_MIN_OFFLOAD_KIB", 0)
+    small = [np.full(64 << 10, i, np.uint8) for i in range(k + m)]
+    d["encode"](k, m, 8, ints(M), ptrs(small[:k]), ptrs(small[k:]), 64 << 10)
+    assert d["decode"](k, m, 8, ints(M), 0, ints([0, 1, 2, 3, -1]), ptrs(small[:k]), ptrs(small[k:]), 64 << 10) == 0
+    core.ecgpu_reset_knob.argtypes = [ctypes.c_char_p]
+    core.ecgpu_reset_knob(b"ECGPU_MIN_OFFLOAD_KIB")
+    print("oom: library warm", file=sys.stderr, flush=True)
+    held, keep = fill_hbm(hip)
+    run.held = held
+    print(f"oom: {held >> 20} MiB of HBM held", file=sys.stderr, flush=True)
     slab = np.zeros((k + m) * size, np.uint8)
     sh = [slab[i * size:(i + 1) * size] for i in range(k + m)]
     for i in range(k):
@@ -356,6 +374,8 @@ def oom(d, core, golden, run):
 
 
 def main():
+    import faulthandler
+    faulthandler.enable()  # a crash names the line it happened on
     scenario = sys.argv[1]
     with open(os.path.join(TESTS, "golden", "golden.json")) as fh:
         golden = json.load(fh)

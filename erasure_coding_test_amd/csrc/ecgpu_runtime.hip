@@ -103,6 +103,11 @@ int fail_hip(hipError_t e, const char* what) {
     (void)hipGetLastError();
   }
   if (lost && d >= 0) mark_device_lost(d);
+  // The library reports the error through its own channel; HIP's per-thread
+  // last error is shared with the caller's HIP code in the same process, so
+  // a handled failure (a bad ordinal, an OOM the CPU completed) must not
+  // surface in the caller's next error check (torch's launch checks did).
+  (void)hipGetLastError();
   return fail(ECGPU_ERR_HIP, msg);
 }
 

@@ -213,3 +213,23 @@ def test_bad_device_ordinal_does_not_mark_a_device_lost_gpu(gpu):
     assert N.lib.ecgpu_device_pci_bus_id(99, buf, 64) == N.ECGPU_ERR_HIP
     assert N.lib.ecgpu_device_lost(0) == 0
     assert N.lib.ecgpu_device_pci_bus_id(0, buf, 64) == 0
+
+
+@pytest.mark.gpu
+def test_handled_hip_error_does_not_leak_into_the_callers_hip_state_gpu(gpu):
+    """A HIP error the library handled (a bad ordinal here; an OOM completed on
+    the CPU in deployment) is cleared from HIP's per-thread last error, which
+    the caller's own HIP code in the same process shares: torch's next launch
+    check used to raise the library's stale 'invalid device ordinal'."""
+    import ctypes
+
+    import torch
+
+    from erasure_coding_test_amd import _native as N
+    buf = ctypes.create_string_buffer(64)
+    assert N.lib.ecgpu_device_pci_bus_id(99, buf, 64) == N.ECGPU_ERR_HIP
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    assert hip.hipPeekAtLastError() == 0
+    t = torch.full((4096,), 7, dtype=torch.uint8, device=gpu)
+    torch.cuda.synchronize()
+    assert int(t.sum()) == 7 * 4096

@@ -54,6 +54,11 @@ def main():
     ap.add_argument("--passes", type=int, default=3)
     ap.add_argument("--legs", default="h2d,d2h,duplex,pipe_encode,pipe_decode")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--pre", type=int, default=0,
+                    help="before the legs: this many bench-step encode launches over a 96-stripe 4 MiB slab "
+                         "(5.3 GiB resident, as bench.py's ranks hold when their e2e leg starts)")
+    ap.add_argument("--bench-data", action="store_true",
+                    help="fill the host stripes like bench.py's e2e leg (one random stripe, copied from HBM)")
     a = ap.parse_args()
 
     import torch
@@ -66,8 +71,24 @@ def main():
     torch.cuda.set_device(dev)
     k, m, S, n = 10, 4, 4 << 20, a.stripes
     M = E.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
+    keep = None
+    if a.pre:
+        slab, shards = E.alloc_stripes(96, k, m, S)
+        slab.random_(0, 256)
+        plan = E.encode_plan(k, m, M).bind([st[:k] for st in shards], [st[k:] for st in shards], S)
+        for _ in range(a.pre):
+            plan.launch()
+        torch.cuda.synchronize(dev)
+        keep = (slab, shards, plan)  # held, like the bench's slab
     host = torch.empty((n, k + m, S), dtype=torch.uint8).pin_memory()
-    host[:, :k].random_(0, 256)
+    if a.bench_data:
+        src = torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev)
+        for s in range(n):
+            host[s, :k].copy_(src)
+            host[s, 0, :8].fill_(s)
+        torch.cuda.synchronize(dev)
+    else:
+        host[:, :k].random_(0, 256)
     for s in range(n):  # valid codewords, so the decode legs have consistent survivors
         d = host[s, :k].to(dev)
         par = torch.empty((m, S), dtype=torch.uint8, device=dev)
@@ -162,6 +183,7 @@ def main():
                               "per_rank_pass_ms": [r["pass_ms"] for r in allr],
                               "ok": [r["ok"] for r in allr]}), flush=True)
     assert N.fallback_count() == 0 and N.cpu_call_count() == 0
+    del keep
     dist.barrier()
     dist.destroy_process_group()
 

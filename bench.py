@@ -1044,22 +1044,29 @@ def main(argv=None):
         mix_dec = xor_stream_probe(slab, S, k, 1)  # every C3 decode shape reads 10 shards and writes 1
         for name in ("C3_decode_0", "C3_decode_data_random", "C3_decode_parity"):
             with_mix(main_entries.get(name), mix_dec)
+    # diagnostics only (A/B of the N > 1 e2e leg): ECGPU_BENCH_SKIP=configs,c5 drops those blocks
+    skip = set(filter(None, os.environ.get("ECGPU_BENCH_SKIP", "").split(",")))
     configs = None
-    if not args.no_configs:
+    if not args.no_configs and "configs" not in skip:
         del shards
         slab = None
         torch.cuda.empty_cache()
         configs = config_block(E, N, dev, stream, kind, bool(args.nt), main_entries)
     c5 = None
-    if not args.no_configs and args.config == "C3":
+    if not args.no_configs and args.config == "C3" and "c5" not in skip:
         c5 = sharded_c5(E, N, dev, stream, kind, bool(args.nt), rank, world)
     # about 1.5 GiB of pinned host memory per rank at most (C3: 24 stripes, C5: 6)
     e2e_n = min(args.e2e_stripes, max(2, (3 << 29) // ((k + m) * S)))
     e2e_mine = None
     if world > 1 and args.e2e_stripes > 0:
-        barrier(world)
-        e2e_mine = e2e_all_ranks(E, M, k, m, S, erasures, dev, local, world, e2e_n)
-        barrier(world)
+        repeats = []
+        for _ in range(max(1, int(os.environ.get("ECGPU_BENCH_E2E_REPEAT", "1") or 1))):  # diagnostics: >1 repeats
+            barrier(world)
+            e2e_mine = e2e_all_ranks(E, M, k, m, S, erasures, dev, local, world, e2e_n)
+            barrier(world)
+            repeats.append({leg: e2e_mine[leg]["pass_ms"] for leg in ("encode", "decode") if leg in e2e_mine})
+        if len(repeats) > 1:
+            e2e_mine["repeats_pass_ms"] = repeats
 
     enc_frac = enc_bytes / (enc_ms / 1e3) / 1e9 / HBM_PEAK_GBS
     mine = {"rank": rank, "device": local, **device_identity(N, local), "elapsed_s": round(elapsed, 6),

@@ -57,6 +57,11 @@ def main():
     ap.add_argument("--pre", type=int, default=0,
                     help="before the legs: this many bench-step encode launches over a 96-stripe 4 MiB slab "
                          "(5.3 GiB resident, as bench.py's ranks hold when their e2e leg starts)")
+    ap.add_argument("--c5", action="store_true",
+                    help="before the legs: bench.py's sharded_c5 on this rank (24 RS(12,4) 16 MiB stripes = 6 GiB, "
+                         "13 encode launches, the slab freed and torch.cuda.empty_cache())")
+    ap.add_argument("--churn-gib", type=int, default=0,
+                    help="before the legs: allocate this many GiB of HBM, fill it, free it and empty torch's cache")
     ap.add_argument("--bench-data", action="store_true",
                     help="fill the host stripes like bench.py's e2e leg (one random stripe, copied from HBM)")
     a = ap.parse_args()
@@ -80,6 +85,23 @@ def main():
             plan.launch()
         torch.cuda.synchronize(dev)
         keep = (slab, shards, plan)  # held, like the bench's slab
+    if a.c5:
+        M5 = E.reed_sol.reed_sol_vandermonde_coding_matrix(12, 4, 8)
+        slab5, sh5 = E.alloc_stripes(24, 12, 4, 16 << 20)
+        slab5.random_(0, 256)
+        p5 = E.encode_plan(12, 4, M5).bind([st[:12] for st in sh5], [st[12:] for st in sh5], 16 << 20)
+        for _ in range(13):
+            p5.launch()
+        torch.cuda.synchronize(dev)
+        p5.close()
+        del slab5, sh5
+        torch.cuda.empty_cache()
+    if a.churn_gib:
+        junk = torch.empty(a.churn_gib << 30, dtype=torch.uint8, device=dev)
+        junk.fill_(1)
+        torch.cuda.synchronize(dev)
+        del junk
+        torch.cuda.empty_cache()
     host = torch.empty((n, k + m, S), dtype=torch.uint8).pin_memory()
     if a.bench_data:
         src = torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev)

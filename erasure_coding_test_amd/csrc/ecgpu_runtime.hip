@@ -585,9 +585,16 @@ int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>&
     if (b - a >= 2 && size_t(pitch) != bytes && !is_pinned(hp[b - 1] + bytes - 1)) b = a + 1;
     uint8_t* d = d0 + a * dstride;
     if (b - a >= 2) {
+      // contiguous on both sides: one 1-D copy.  HIP's 2-D copies lost 40 % of
+      // the link when two processes shared the GPU in some allocation states
+      // (bench.py's N = 2 rehearsal after its C5 leg: 27 vs 44 GiB/s; 1-D
+      // copies 41)
+      const bool flat = size_t(pitch) == bytes && dstride == bytes;
       const hipError_t e =
-          h2d ? hipMemcpy2DAsync(d, dstride, hp[a], size_t(pitch), bytes, b - a, hipMemcpyHostToDevice, s)
-              : hipMemcpy2DAsync(hp[a], size_t(pitch), d, dstride, bytes, b - a, hipMemcpyDeviceToHost, s);
+          flat ? (h2d ? hipMemcpyAsync(d, hp[a], bytes * (b - a), hipMemcpyHostToDevice, s)
+                      : hipMemcpyAsync(hp[a], d, bytes * (b - a), hipMemcpyDeviceToHost, s))
+          : h2d ? hipMemcpy2DAsync(d, dstride, hp[a], size_t(pitch), bytes, b - a, hipMemcpyHostToDevice, s)
+                : hipMemcpy2DAsync(hp[a], size_t(pitch), d, dstride, bytes, b - a, hipMemcpyDeviceToHost, s);
       if (e == hipSuccess) {
         a = b;
         continue;

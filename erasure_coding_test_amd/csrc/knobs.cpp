@@ -58,6 +58,7 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_MIN_OFFLOAD_KIB", "min_offload_kib", 16384},
     {"ECGPU_CPU_SIMD", "cpu_simd", -1},
     {"ECGPU_PIPE_ZC", "pipe_zc", 0},
+    {"ECGPU_PIPE_CONTIG", "pipe_contig", 1},
 };
 
 constexpr int kUnset = INT_MIN;

@@ -55,6 +55,8 @@ enum class Knob : int {
   kPipeZc,          // ECGPU_PIPE_ZC: host pipelines over pinned host shards -- 0 DMA in and out, 1 DMA in and
                     // the kernel writes the outputs into the pinned host buffers, 2 the kernel reads the
                     // sources and writes the outputs in host memory (no DMA); read at pipeline creation
+  kPipeContig,      // ECGPU_PIPE_CONTIG: host pipelines lay a ring slot's shards back to back (size % 256 == 0),
+                    // so contiguous host stripes move as one 1-D copy; 0 = the skewed shard stride (read at creation)
   kCount
 };
 

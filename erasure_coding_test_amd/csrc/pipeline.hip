@@ -194,7 +194,13 @@ ecgpu_pipeline* pipeline_build(int k, int m, int rows, int nsrc, const int* coef
   d.size = size;
   d.src_ids.assign(src_ids, src_ids + nsrc);
   d.out_ids.assign(out_ids, out_ids + rows);
-  d.slot_stride = size_t(ecgpu_recommended_shard_stride_km(size, k, m));
+  // ECGPU_PIPE_CONTIG (default 1): a slot's shards back to back when the size
+  // keeps them 256-B aligned, so a stripe laid out contiguously in host memory
+  // crosses PCIe as one 1-D copy each way (copy_shards); the shard-stride skew
+  // (§4) buys a few us of a one-stripe launch that hides under a 0.8 ms copy
+  d.slot_stride = knob(Knob::kPipeContig) != 0 && size % 256 == 0
+                      ? size_t(size)
+                      : size_t(ecgpu_recommended_shard_stride_km(size, k, m));
   DeviceGuard g(d.device);
   auto bad = [&](hipError_t e, const char* what) {
     fail(ECGPU_ERR_HIP, std::string("ecgpu_pipeline: ") + what + ": " + hipGetErrorString(e));

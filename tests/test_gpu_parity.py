@@ -728,13 +728,16 @@ def test_host_pipeline_wait_is_exact_with_delayed_worker(ec, gpu, restatement, d
 
 @pytest.mark.parametrize("pinned", [True, False])
 @pytest.mark.parametrize("pitch_pad", [0, 4096 + 3])
-def test_host_pipeline_stripe_slab(ec, gpu, restatement, pinned, pitch_pad):
+@pytest.mark.parametrize("size", [(1 << 20) + 7, 1 << 20])
+def test_host_pipeline_stripe_slab(ec, gpu, restatement, pinned, pitch_pad, size):
     """Stripes laid out in one host slab (evenly spaced shards, as the
     reference client's stripe buffer): the pipeline moves each direction as
-    ONE 2-D copy.  Encode, then a decode pipeline over the same slab with two
+    ONE copy -- 2-D into skewed ring slots, or 1-D when the slab is contiguous
+    and the size lets the ring slots be contiguous (ECGPU_PIPE_CONTIG, 256-B
+    multiples).  Encode, then a decode pipeline over the same slab with two
     data shards and one parity shard erased, against the oracle."""
     import torch
-    k, m, size, stripes = 10, 4, (1 << 20) + 7, 5
+    k, m, stripes = 10, 4, 5
     pitch = size + pitch_pad
     M = ec.reed_sol.reed_sol_vandermonde_coding_matrix(k, m, 8)
     slab = torch.zeros((stripes, k + m, pitch), dtype=torch.uint8)

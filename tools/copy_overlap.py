@@ -78,7 +78,8 @@ def main():
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--h2d-bytes", type=int, default=10 * (4 << 20))
     ap.add_argument("--d2h-bytes", type=int, default=4 * (4 << 20))
-    ap.add_argument("--min-bytes-us", type=float, default=0.0)
+    ap.add_argument("--skip-null-stream", action="store_true",
+                    help="ignore copies on stream 0 (a script's own setup copies through torch's null stream)")
     a = ap.parse_args()
     size = {"h2d": a.h2d_bytes, "d2h": a.d2h_bytes}
     copies = []  # per process: {dir: [(s, e)]}
@@ -87,6 +88,8 @@ def main():
         per = {"h2d": [], "d2h": []}
         for r in load(d, "memory_copy_trace.csv"):
             k = direction(r)
+            if a.skip_null_stream and str(r.get("Stream_Id", "")).strip() == "0":
+                continue
             if k:
                 per[k].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
         copies.append(per)

@@ -20,6 +20,8 @@ Legs (per rank, `stripes` stripes of pinned host memory [stripes][k+m][S]):
                into the pinned host stripes in place (no D2H DMA)
   pipe_*_zc2   ECGPU_PIPE_ZC=2: the kernel also reads the sources in place
                (no DMA at all)
+  pipe_*_skew  ECGPU_PIPE_CONTIG=0: ring slots at the skewed shard stride, so
+               each stripe moves as 2-D copies (the round-5 layout)
 Pipeline legs check the last stripe after the last pass (its outputs zeroed
 before it): encode parity against a device-resident encode, decode against
 the original shard.
@@ -152,19 +154,22 @@ def main():
 
     from erasure_coding_test_amd import _native as N
 
-    def pipeline(decode, zc):
+    def pipeline(decode, zc, contig=1):
         def make():
             N.set_knob("pipe_zc", zc)  # read at creation
+            N.set_knob("pipe_contig", contig)
             p = (E.HostPipeline.decoder(k, m, M, [0], S, depth=a.depth, device=0) if decode
                  else E.HostPipeline(k, m, M, S, depth=a.depth, device=0))
             N.reset_knob("pipe_zc")
+            N.reset_knob("pipe_contig")
             return p
         return None, make
 
     legs = {"h2d": (h2d, None), "d2h": (d2h, None), "duplex": (duplex, None),
             "pipe_encode": pipeline(False, 0), "pipe_decode": pipeline(True, 0),
             "pipe_encode_zc1": pipeline(False, 1), "pipe_encode_zc2": pipeline(False, 2),
-            "pipe_decode_zc1": pipeline(True, 1), "pipe_decode_zc2": pipeline(True, 2)}
+            "pipe_decode_zc1": pipeline(True, 1), "pipe_decode_zc2": pipeline(True, 2),
+            "pipe_encode_skew": pipeline(False, 0, 0), "pipe_decode_skew": pipeline(True, 0, 0)}
     for name in a.legs.split(","):
         fn, make = legs[name]
         p = make() if make else None

@@ -64,6 +64,8 @@ def main():
                          "13 encode launches, the slab freed and torch.cuda.empty_cache())")
     ap.add_argument("--churn-gib", type=int, default=0,
                     help="before the legs: allocate this many GiB of HBM, fill it, free it and empty torch's cache")
+    ap.add_argument("--knob", action="append", default=[],
+                    help="name=value: a library knob for the whole run (ecgpu_set_knob), e.g. ECGPU_ZC_GRID=256")
     ap.add_argument("--bench-data", action="store_true",
                     help="fill the host stripes like bench.py's e2e leg (one random stripe, copied from HBM)")
     a = ap.parse_args()
@@ -153,6 +155,9 @@ def main():
         return run
 
     from erasure_coding_test_amd import _native as N
+    for kv in a.knob:
+        name, value = kv.split("=")
+        N.set_knob(name, int(value))
 
     def pipeline(decode, zc, contig=1):
         def make():

@@ -48,6 +48,7 @@ SIGNATURES = {
     "ecgpu_free": (None, [c_void_p]),
     "ecgpu_fallback_count": (c_int64, []),
     "ecgpu_cpu_call_count": (c_int64, []),
+    "ecgpu_min_offload_bytes": (c_int64, []),
     "ecgpu_device_lost": (c_int, [c_int]),
     "ecgpu_set_devices": (c_int, [c_int, c_int_p]),
     "ecgpu_get_devices": (c_int, [c_int_p, c_int]),

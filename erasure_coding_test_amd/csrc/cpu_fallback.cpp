@@ -3,6 +3,7 @@
 // executor (cpu_exec.cpp) by choice.
 #include "cpu_fallback.hpp"
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <mutex>
@@ -67,10 +68,19 @@ void record_fallback(const char* call, const std::string& why) {
 
 int64_t fallback_count() { return g_fallbacks.load(std::memory_order_relaxed); }
 
+// The crossover per executor SIMD level (tools/crossover.cpp on the MI355X
+// host, scored by tools/crossover_fit.py: profiles/r06_crossover_fit.txt,
+// r06_crossover_simd.txt): GFNI 16 MiB, AVX2 4 MiB, scalar 256 KiB.
+int64_t min_offload_bytes() {
+  const int kib = knob(Knob::kMinOffloadKib);
+  if (kib >= 0) return int64_t(kib) << 10;
+  static const int64_t by_level[3] = {int64_t(256) << 10, int64_t(4) << 20, int64_t(16) << 20};
+  return by_level[std::max(0, std::min(2, cpu_simd_level()))];
+}
+
 bool cpu_by_choice(int64_t bytes_moved) {
   if (knob(Knob::kGpu) == 0) return true;
-  const int kib = knob(Knob::kMinOffloadKib);
-  return kib > 0 && bytes_moved < (int64_t(kib) << 10);
+  return bytes_moved < min_offload_bytes();
 }
 
 void record_cpu_call() { g_cpu_calls.fetch_add(1, std::memory_order_relaxed); }
@@ -83,5 +93,6 @@ int64_t cpu_call_count() { return g_cpu_calls.load(std::memory_order_relaxed); }
 extern "C" {
 ECGPU_API int64_t ecgpu_fallback_count(void) { return ecgpu::rt::fallback_count(); }
 ECGPU_API int64_t ecgpu_cpu_call_count(void) { return ecgpu::rt::cpu_call_count(); }
+ECGPU_API int64_t ecgpu_min_offload_bytes(void) { return ecgpu::rt::min_offload_bytes(); }
 ECGPU_API int ecgpu_device_lost(int device) { return ecgpu::rt::device_lost(device) ? 1 : 0; }
 }

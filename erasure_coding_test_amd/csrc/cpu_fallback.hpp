@@ -64,6 +64,8 @@ int64_t fallback_count();
 // Does a host-memory call moving `bytes_moved` bytes run on the CPU executor
 // by choice (ECGPU_GPU=0, or below ECGPU_MIN_OFFLOAD_KIB)?
 bool cpu_by_choice(int64_t bytes_moved);
+// The threshold in force (ecgpu_min_offload_bytes).
+int64_t min_offload_bytes();
 void record_cpu_call();
 int64_t cpu_call_count();
 

@@ -55,7 +55,7 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_CPU_FALLBACK", "cpu_fallback", 1},
     {"ECGPU_TEST_INJECT_HIP", "test_inject_hip", 0, true},
     {"ECGPU_GPU", "gpu", 1},
-    {"ECGPU_MIN_OFFLOAD_KIB", "min_offload_kib", 16384},
+    {"ECGPU_MIN_OFFLOAD_KIB", "min_offload_kib", -1},
     {"ECGPU_CPU_SIMD", "cpu_simd", -1},
     {"ECGPU_PIPE_ZC", "pipe_zc", 0},
     {"ECGPU_PIPE_CONTIG", "pipe_contig", 1},

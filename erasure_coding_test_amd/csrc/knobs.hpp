@@ -48,8 +48,9 @@ enum class Knob : int {
                     // the device marked lost, 3 after writing caller memory
   kGpu,             // ECGPU_GPU: 0 runs every synchronous host-memory call on the CPU executor (cpu_exec.hpp)
   kMinOffloadKib,   // ECGPU_MIN_OFFLOAD_KIB: a synchronous host-memory call moving fewer bytes (distinct
-                    // buffers x size) runs on the CPU executor; 0 = every call on the GPU.  Default 16 MiB:
-                    // the rule with the least slowdown over tools/crossover.cpp's grid
+                    // buffers x size) runs on the CPU executor; 0 = every call on the GPU; -1 (default) = the
+                    // measured crossover for the executor's SIMD level, 16 MiB GFNI / 4 MiB AVX2 / 256 KiB
+                    // scalar (cpu_fallback.cpp min_offload_bytes)
   kCpuSimd,         // ECGPU_CPU_SIMD: the CPU executor's SIMD level, -1 the host's best, 2 AVX-512 + GFNI,
                     // 1 AVX2, 0 scalar (never above what the host has)
   kPipeZc,          // ECGPU_PIPE_ZC: host pipelines over pinned host shards -- 0 DMA in and out, 1 DMA in and

@@ -20,8 +20,9 @@
  * (classified per buffer; host buffers are staged through HBM) and are
  * synchronous: results are valid on return, like the reference.  A call
  * whose buffers are all host memory and that moves fewer than
- * ECGPU_MIN_OFFLOAD_KIB bytes (distinct buffers x size; 16 MiB by default,
- * the measured crossover of DESIGN.md §8; every such call with ECGPU_GPU=0)
+ * ECGPU_MIN_OFFLOAD_KIB bytes (distinct buffers x size; by default the
+ * measured crossover for the host's SIMD level, 16 MiB with GFNI,
+ * ecgpu_min_offload_bytes; every such call with ECGPU_GPU=0)
  * runs on the library's own CPU executor, where the GPU round trip would
  * cost more (counted by ecgpu_cpu_call_count).  A HIP failure on
  * a call whose buffers are all host memory, before it overwrote one of its
@@ -92,6 +93,11 @@ ECGPU_API int ecgpu_device_lost(int device);
 /* Synchronous host-memory calls run on the CPU executor by choice: below
  * ECGPU_MIN_OFFLOAD_KIB, or with ECGPU_GPU=0 (process total). */
 ECGPU_API int64_t ecgpu_cpu_call_count(void);
+/* The bytes-moved threshold in force (0: every call to the GPU): the
+ * ECGPU_MIN_OFFLOAD_KIB knob when set, else by the executor's SIMD level --
+ * 16 MiB with AVX-512 + GFNI, 4 MiB with AVX2, 256 KiB scalar, each the
+ * measured crossover on the MI355X host. */
+ECGPU_API int64_t ecgpu_min_offload_bytes(void);
 /* The devices synchronous host-memory calls spread over (default: unset, the
  * caller's current device).  Each calling thread is given one entry,
  * round-robin in the order threads make their first such call, and keeps it,

@@ -119,15 +119,37 @@ def test_ecx_block_sequence_below_default_threshold():
     the GPU untouched and the fallback off they complete, bit-exact."""
     _need_reference()
     code = ("from erasure_coding_test_amd import _native as N\n"
-            "import ctypes; v = ctypes.c_int(); N.lib.ecgpu_reset_knob(b'ECGPU_MIN_OFFLOAD_KIB')\n"
-            "N.lib.ecgpu_get_knob(b'ECGPU_MIN_OFFLOAD_KIB', ctypes.byref(v)); print(v.value)\n")
+            "N.lib.ecgpu_reset_knob(b'ECGPU_MIN_OFFLOAD_KIB')\n"
+            "print(N.lib.ecgpu_min_offload_bytes())\n")
     r = run_py(code)
-    default_kib = int(r.stdout.split()[-1])
-    assert default_kib > 0, "the library's default threshold must be a measured crossover, not 0"
+    default_bytes = int(r.stdout.split()[-1])
+    assert default_bytes > 0, "the library's default threshold must be a measured crossover, not 0"
     r, out = drive("ecx")
-    if 2 * 349525 < default_kib * 1024:
+    if 2 * 349525 < default_bytes:
         assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
         assert out["mismatches"] == [] and out["fallbacks"] == 0 and out["cpu_calls"] > 0, out
+
+
+def test_default_threshold_follows_the_executor_simd_level():
+    """ECGPU_MIN_OFFLOAD_KIB unset (-1): the measured crossover for the
+    executor's SIMD level (GFNI 16 MiB, AVX2 4 MiB, scalar 256 KiB, DESIGN.md
+    §8); a set value wins; the Python package's 0 sends everything to the GPU."""
+    code = ("import ctypes, os\n"
+            "from erasure_coding_test_amd import _native as N\n"
+            "N.lib.ecgpu_reset_knob(b'ECGPU_MIN_OFFLOAD_KIB')\n"
+            "lvl = ctypes.c_int(); N.lib.ecgpu_get_knob(b'ECGPU_CPU_SIMD', ctypes.byref(lvl))\n"
+            "print('auto', N.lib.ecgpu_min_offload_bytes())\n"
+            "N.set_knob('ECGPU_MIN_OFFLOAD_KIB', 100); print('set', N.lib.ecgpu_min_offload_bytes())\n"
+            "N.reset_knob('ECGPU_MIN_OFFLOAD_KIB'); print('package', N.lib.ecgpu_min_offload_bytes())\n")
+    want = {"0": 256 << 10, "1": 4 << 20}
+    for level in ("0", "1"):
+        r = run_py(code, ECGPU_CPU_SIMD=level)
+        assert r.returncode == 0, r.stderr[-2000:]
+        got = dict(line.split() for line in r.stdout.splitlines() if line.split()[0] in ("auto", "set", "package"))
+        assert int(got["auto"]) == want[level] and int(got["set"]) == 100 << 10 and int(got["package"]) == 0, got
+    r = run_py(code)  # the host's best level: GFNI hosts 16 MiB
+    got = dict(line.split() for line in r.stdout.splitlines() if line.split()[0] in ("auto", "set", "package"))
+    assert int(got["auto"]) in (256 << 10, 4 << 20, 16 << 20), got
 
 
 def test_gpu_switch_does_not_touch_device_memory_logic():

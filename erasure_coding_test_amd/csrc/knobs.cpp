@@ -23,6 +23,7 @@ struct KnobDef {
   const char* name;
   int dflt;
   bool set_only = false;  // settable only through ecgpu_set_knob (test hooks: never from a deployment's environment)
+  const char* alias = nullptr;  // a second environment name, read when `env` is unset
 };
 
 // Defaults are the production choices (measured).
@@ -54,7 +55,7 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {nullptr, "test_d2h_delay_us", 0},
     {"ECGPU_CPU_FALLBACK", "cpu_fallback", 1},
     {"ECGPU_TEST_INJECT_HIP", "test_inject_hip", 0, true},
-    {"ECGPU_GPU", "gpu", 1},
+    {"ECGPU_GPU", "gpu", 1, false, "EC_GPU"},  // EC_GPU=0/1: SURVEY §5's switch
     {"ECGPU_MIN_OFFLOAD_KIB", "min_offload_kib", -1},
     {"ECGPU_CPU_SIMD", "cpu_simd", -1},
     {"ECGPU_PIPE_ZC", "pipe_zc", 0},
@@ -69,6 +70,7 @@ std::atomic<int> g_over[int(Knob::kCount)];   // ecgpu_set_knob's value, kUnset 
 // A whole-string decimal integer, else the default (so "", "x", "12k" keep it).
 int parse_env(const KnobDef& d) {
   const char* e = d.env && !d.set_only ? std::getenv(d.env) : nullptr;
+  if ((!e || !*e) && d.alias && !d.set_only) e = std::getenv(d.alias);
   if (!e || !*e) return d.dflt;
   errno = 0;
   char* end = nullptr;

@@ -39,7 +39,7 @@ def _need_reference():
 
 def _env(**kw):
     env = {k: v for k, v in os.environ.items()
-           if k not in ("ECGPU_GPU", "ECGPU_MIN_OFFLOAD_KIB", "ECGPU_CPU_SIMD", "ECGPU_TEST_INJECT_HIP")}
+           if k not in ("ECGPU_GPU", "EC_GPU", "ECGPU_MIN_OFFLOAD_KIB", "ECGPU_CPU_SIMD", "ECGPU_TEST_INJECT_HIP")}
     env["ECGPU_CPU_FALLBACK"] = "0"  # nothing may reach the CPU through the fallback here
     env.update({k: str(v) for k, v in kw.items()})
     return env
@@ -150,6 +150,16 @@ def test_default_threshold_follows_the_executor_simd_level():
     r = run_py(code)  # the host's best level: GFNI hosts 16 MiB
     got = dict(line.split() for line in r.stdout.splitlines() if line.split()[0] in ("auto", "set", "package"))
     assert int(got["auto"]) in (256 << 10, 4 << 20, 16 << 20), got
+
+
+def test_ec_gpu_alias_of_the_gpu_switch():
+    """SURVEY §5 names the switch EC_GPU=0/1: it sets ECGPU_GPU when that is
+    unset; ECGPU_GPU wins when both are set."""
+    code = ("from erasure_coding_test_amd import _native as N\n"
+            "print('gpu', N.get_knob('ECGPU_GPU'))\n")
+    for env, want in (({"EC_GPU": "0"}, 0), ({"EC_GPU": "1"}, 1), ({"EC_GPU": "0", "ECGPU_GPU": "1"}, 1), ({}, 1)):
+        r = run_py(code, **env)
+        assert r.returncode == 0 and f"gpu {want}" in r.stdout, (env, r.stdout, r.stderr[-2000:])
 
 
 def test_gpu_switch_does_not_touch_device_memory_logic():

@@ -590,13 +590,9 @@ int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>&
       // (bench.py's N = 2 rehearsal after its C5 leg: 27 vs 44 GiB/s; 1-D
       // copies 41)
       const bool flat = size_t(pitch) == bytes && dstride == bytes;
-      // ECGPU_D2H_NOCU: a device -> pinned D2H as a "device to device, no
-      // compute units" copy (SDMA) instead of HIP's blit kernel
-      const hipMemcpyKind d2h_kind =
-          knob(Knob::kD2hNoCu) != 0 && is_pinned(hp[a]) ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost;
       const hipError_t e =
           flat ? (h2d ? hipMemcpyAsync(d, hp[a], bytes * (b - a), hipMemcpyHostToDevice, s)
-                      : hipMemcpyAsync(hp[a], d, bytes * (b - a), d2h_kind, s))
+                      : hipMemcpyAsync(hp[a], d, bytes * (b - a), hipMemcpyDeviceToHost, s))
           : h2d ? hipMemcpy2DAsync(d, dstride, hp[a], size_t(pitch), bytes, b - a, hipMemcpyHostToDevice, s)
                 : hipMemcpy2DAsync(hp[a], size_t(pitch), d, dstride, bytes, b - a, hipMemcpyDeviceToHost, s);
       if (e == hipSuccess) {

@@ -60,7 +60,6 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_CPU_SIMD", "cpu_simd", -1},
     {"ECGPU_PIPE_ZC", "pipe_zc", 0},
     {"ECGPU_PIPE_CONTIG", "pipe_contig", 1},
-    {"ECGPU_D2H_NOCU", "d2h_nocu", 0},
 };
 
 constexpr int kUnset = INT_MIN;

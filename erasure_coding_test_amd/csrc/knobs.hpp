@@ -58,8 +58,6 @@ enum class Knob : int {
                     // sources and writes the outputs in host memory (no DMA); read at pipeline creation
   kPipeContig,      // ECGPU_PIPE_CONTIG: host pipelines lay a ring slot's shards back to back (size % 256 == 0),
                     // so contiguous host stripes move as one 1-D copy; 0 = the skewed shard stride (read at creation)
-  kD2hNoCu,         // ECGPU_D2H_NOCU: flat D2H copies into pinned memory (copy_shards) as hipMemcpyDeviceToDeviceNoCU
-                    // (an SDMA engine) instead of HIP's D2H blit kernel; 0 = HIP's choice
   kCount
 };
 

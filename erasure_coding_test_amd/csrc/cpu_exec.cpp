@@ -54,6 +54,27 @@ Nib8 nib8(uint32_t c) {
   return t;
 }
 
+// Per-coefficient tables of GF(2^8), built once: the affine matrix of
+// y -> c * y (vgf2p8affineqb) and the nibble tables -- a call's setup then
+// costs lookups, not 64-step bit scatters per coefficient (the whole fixed
+// cost of a small call's execution).
+struct W8Tables {
+  uint64_t affine[256];
+  Nib8 nib[256];
+};
+
+const W8Tables& w8_tables() {
+  static const W8Tables t = [] {
+    W8Tables x{};
+    for (uint32_t c = 0; c < 256; ++c) {
+      x.affine[c] = gf_affine_block(c, 8, 0, 0);
+      x.nib[c] = nib8(c);
+    }
+    return x;
+  }();
+  return t;
+}
+
 // ================================================ AVX-512 + GFNI ====
 inline __mmask64 tail_mask(int64_t n) { return n >= 64 ? ~__mmask64(0) : (__mmask64(1) << n) - 1; }
 
@@ -241,7 +262,11 @@ std::vector<Group> plan_groups(const FusedOp& op, int level) {
       for (int r = 0; r < g.R; ++r) {
         const uint32_t c = op.coef[size_t(r0 + r) * nsrc + j] & mask;
         if (level < 2) {
-          g.T.push_back(nib8(c));
+          g.T.push_back(w8_tables().nib[c & 0xFFu]);
+          continue;
+        }
+        if (op.w == 8) {
+          g.A.push_back(w8_tables().affine[c]);
           continue;
         }
         for (int s = 0; s < B; ++s)
@@ -260,11 +285,18 @@ void run_group(const FusedOp& op, const Group& g, int64_t off, uint8_t* const* d
     for (int r = 0; r < g.R; ++r) std::memset(dst[r], 0, size_t(n));
     return;
   }
-  std::vector<const uint8_t*> src(g.js.size());
+  const uint8_t* small[32];  // no allocation for the usual source counts
+  std::vector<const uint8_t*> big;
+  const uint8_t** src = small;
+  if (g.js.size() > 32) {
+    big.resize(g.js.size());
+    src = big.data();
+  }
   for (size_t i = 0; i < g.js.size(); ++i) src[i] = static_cast<const uint8_t*>(op.srcs[size_t(g.js[i])]) + off;
-  if (level >= 2) return gfni_group(g.R, op.w)(src.data(), int(src.size()), dst, g.A.data(), n);
+  const int K = int(g.js.size());
+  if (level >= 2) return gfni_group(g.R, op.w)(src, K, dst, g.A.data(), n);
   static const Avx2GroupFn t8[kRows] = {avx2_group8<1>, avx2_group8<2>, avx2_group8<3>, avx2_group8<4>};
-  t8[g.R - 1](src.data(), int(src.size()), dst, g.T.data(), n);
+  t8[g.R - 1](src, K, dst, g.T.data(), n);
 }
 
 // Row groups of <= kRows outputs, each one pass over its sources (level 2:
@@ -376,7 +408,7 @@ void apply_nibbles(const FusedOp& op, int64_t size, int level) {
     Term& t = terms[i];
     t.c = op.coef[i] & mask;
     if (t.c <= 1) continue;
-    if (op.w == 8) t.t8 = nib8(t.c);
+    if (op.w == 8) t.t8 = w8_tables().nib[t.c & 0xFFu];
     else if (op.w == 16) t.t16 = nibw<uint16_t>(t.c);
     else t.t32 = nibw<uint32_t>(t.c);
   }

@@ -589,7 +589,8 @@ int copy_shards(bool h2d, uint8_t* d0, size_t dstride, const std::vector<char*>&
       // the link when two processes shared the GPU in some allocation states
       // (bench.py's N = 2 rehearsal after its C5 leg: 27 vs 44 GiB/s; 1-D
       // copies 41)
-      const bool flat = size_t(pitch) == bytes && dstride == bytes;
+      // (ECGPU_PIPE_FLAT=0 keeps flat runs on hipMemcpy2DAsync too: an A/B switch)
+      const bool flat = size_t(pitch) == bytes && dstride == bytes && knob(Knob::kPipeFlat) != 0;
       const hipError_t e =
           flat ? (h2d ? hipMemcpyAsync(d, hp[a], bytes * (b - a), hipMemcpyHostToDevice, s)
                       : hipMemcpyAsync(hp[a], d, bytes * (b - a), hipMemcpyDeviceToHost, s))

@@ -1,6 +1,7 @@
 // planner.cpp -- see planner.hpp.
 #include "planner.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "gf_host.hpp"
@@ -9,12 +10,23 @@
 namespace ecgpu {
 
 int LinearTracker::id(void* p) {
-  auto it = idx_.find(p);
-  if (it != idx_.end()) return it->second;
+  // a call names a handful of buffers: a scan beats hashing; the map takes
+  // over for long schedules
+  if (bufs_.size() <= kScanIds) {
+    for (size_t i = 0; i < bufs_.size(); ++i)
+      if (bufs_[i] == p) return static_cast<int>(i);
+  } else {
+    if (idx_.empty())
+      for (size_t i = 0; i < bufs_.size(); ++i) idx_.emplace(bufs_[i], static_cast<int>(i));
+    auto it = idx_.find(p);
+    if (it != idx_.end()) return it->second;
+  }
   const int b = static_cast<int>(bufs_.size());
-  idx_.emplace(p, b);
+  if (!idx_.empty()) idx_.emplace(p, b);
   bufs_.push_back(p);
-  Vec v(bufs_.size(), 0);
+  Vec v;
+  v.reserve(std::max<size_t>(16, bufs_.size()));  // later ids grow it without reallocating
+  v.assign(bufs_.size(), 0);
   v[b] = 1;  // untouched buffer = its own original contents
   state_.push_back(std::move(v));
   written_.push_back(0);
@@ -56,19 +68,24 @@ void LinearTracker::xor3(void* r1, void* r2, void* r3) {
 
 void LinearTracker::mul(void* src, int c, void* dst, bool add) {
   const int s = id(src), d = id(dst);
-  Vec v = state(s);
+  // in place, element by element (no temporary: s == d reads each element
+  // before writing it); both states sized to every registered buffer
+  const size_t n = bufs_.size();
+  const Vec& v = state(s);
+  Vec& out = state(d);
   if (w_ == 8) {
     const auto& T = gf8().mul[c & 0xFF];
-    for (auto& x : v) x = T[x];
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t x = v[i];
+      out[i] = T[x] ^ (add ? out[i] : 0u);
+    }
   } else {
     const uint32_t cw = w_ == 32 ? uint32_t(c) : uint32_t(c) & ((1u << w_) - 1u);
-    for (auto& x : v) x = x ? gf_mul_poly(x, cw, w_) : 0u;
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t x = v[i];
+      out[i] = (x ? gf_mul_poly(x, cw, w_) : 0u) ^ (add ? out[i] : 0u);
+    }
   }
-  if (add) {
-    const Vec& old = state(d);
-    for (size_t i = 0; i < v.size(); ++i) v[i] ^= old[i];
-  }
-  state(d) = std::move(v);
   written_[d] = 1;
 }
 
@@ -102,32 +119,27 @@ void LinearTracker::dotprod(int k, const int* row, const int* src_ids, int dest_
 FusedOp LinearTracker::finish() const {
   FusedOp op;
   const size_t n = bufs_.size();
+  // a state shorter than n has zeros past its end (registered after it was last touched)
+  auto at = [&](size_t b, size_t i) -> uint32_t { return i < state_[b].size() ? state_[b][i] : 0u; };
   std::vector<int> outs;
   for (size_t b = 0; b < n; ++b) {
     if (!written_[b]) continue;
-    Vec v = state_[b];
-    v.resize(n, 0);
-    bool identity = v[b] == 1;
+    bool identity = at(b, b) == 1;
     for (size_t i = 0; identity && i < n; ++i)
-      if (i != b && v[i]) identity = false;
+      if (i != b && at(b, i)) identity = false;
     if (!identity) outs.push_back(static_cast<int>(b));  // unchanged content needs no write
   }
   std::vector<int> col(n, -1);
-  for (int b : outs) {
-    Vec v = state_[b];
-    v.resize(n, 0);
+  for (int b : outs)
     for (size_t i = 0; i < n; ++i)
-      if (v[i] && col[i] < 0) {
+      if (at(size_t(b), i) && col[i] < 0) {
         col[i] = static_cast<int>(op.srcs.size());
         op.srcs.push_back(bufs_[i]);
       }
-  }
   op.coef.assign(outs.size() * op.srcs.size(), 0);
   for (size_t r = 0; r < outs.size(); ++r) {
-    Vec v = state_[outs[r]];
-    v.resize(n, 0);
     for (size_t i = 0; i < n; ++i)
-      if (v[i]) op.coef[r * op.srcs.size() + col[i]] = v[i];
+      if (const uint32_t c = at(size_t(outs[r]), i)) op.coef[r * op.srcs.size() + col[i]] = c;
     op.dsts.push_back(bufs_[outs[r]]);
     if (col[outs[r]] >= 0) op.dst_is_src = true;
   }

@@ -12,6 +12,7 @@
 // sequential reference, including aliasing (a destination that is also a
 // source) and the "all-zero row leaves the destination untouched" rule.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <unordered_map>
 #include <vector>
@@ -64,7 +65,8 @@ class LinearTracker {
   int w_ = 8;
   Vec& state(int b);
   std::vector<void*> bufs_;
-  std::unordered_map<void*, int> idx_;
+  static constexpr std::size_t kScanIds = 32;  // id(): linear scan up to this many buffers, then the map
+  std::unordered_map<void*, int> idx_;     // filled only past kScanIds
   std::vector<Vec> state_;
   std::vector<char> written_;
   double xor_ = 0, gf_ = 0, memcpy_ = 0;

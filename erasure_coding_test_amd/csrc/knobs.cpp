@@ -61,7 +61,6 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_PIPE_ZC", "pipe_zc", 0},
     {"ECGPU_PIPE_CONTIG", "pipe_contig", 1},
     {"ECGPU_PIPE_FLAT", "pipe_flat", 1},
-    {"ECGPU_PIPE_D2H_SPLIT", "pipe_d2h_split", 0},
 };
 
 constexpr int kUnset = INT_MIN;

@@ -58,8 +58,9 @@ enum class Knob : int {
                     // sources and writes the outputs in host memory (no DMA); read at pipeline creation
   kPipeContig,      // ECGPU_PIPE_CONTIG: host pipelines lay a ring slot's shards back to back (size % 256 == 0),
                     // so contiguous host stripes move as one 1-D copy; 0 = the skewed shard stride (read at creation)
-  kPipeFlat,        // ECGPU_PIPE_FLAT: runs contiguous on both sides move as one 1-D copy (copy_shards); 0 = 2-D
-  kPipeD2hSplit,    // ECGPU_PIPE_D2H_SPLIT: host pipelines copy each output shard back on its own (read at creation)
+  kPipeFlat,        // ECGPU_PIPE_FLAT: runs contiguous on both sides move as one 1-D copy (copy_shards); 0 = as a
+                    // 2-D copy anyway (HIP's 2-D device->pinned copy: +4 % for one process, collapsing when
+                    // processes share the GPU)
   kCount
 };
 

@@ -48,7 +48,6 @@ struct PipeDevice {
   // pinned host buffers in place, 2 it also reads the sources there (no DMA);
   // a stripe whose buffers are not all mapped host memory takes the DMA path.
   int zc_mode = 0;
-  bool d2h_per_shard = false;         // ECGPU_PIPE_D2H_SPLIT (read at creation)
   FusedOp zc_op;                      // the map for gf_apply_inl launches (coef only; pointers per stripe)
   std::vector<char> zc_slot;          // per slot: its outputs were written in place (no D2H)
 
@@ -135,15 +134,8 @@ struct PipeDevice {
   // D2H of a slot's outputs (s_d2h, after the slot's compute), then drained.
   int d2h(int sl, const std::vector<char*>& hp) {
     ECGPU_HIP(hipStreamWaitEvent(s_d2h, computed[sl], 0));
-    if (!zc_slot[size_t(sl)]) {  // (written in place by the kernel: nothing to copy)
-      if (d2h_per_shard) {  // ECGPU_PIPE_D2H_SPLIT: one copy per output shard
-        for (size_t i = 0; i < hp.size(); ++i)
-          if (int rc = copy_shards(false, slot_shard(sl, nsrc() + int(i)), slot_stride, {hp[i]}, size_t(size), s_d2h))
-            return rc;
-      } else if (int rc = copy_shards(false, slot_shard(sl, nsrc()), slot_stride, hp, size_t(size), s_d2h)) {
-        return rc;
-      }
-    }
+    if (!zc_slot[size_t(sl)])  // (written in place by the kernel: nothing to copy)
+      if (int rc = copy_shards(false, slot_shard(sl, nsrc()), slot_stride, hp, size_t(size), s_d2h)) return rc;
     ECGPU_HIP(hipEventRecord(drained[sl], s_d2h));
     return ECGPU_OK;
   }
@@ -231,7 +223,6 @@ ecgpu_pipeline* pipeline_build(int k, int m, int rows, int nsrc, const int* coef
   d.zc_op.srcs.assign(size_t(nsrc), nullptr);  // counts only (inline_ok); pointers are per stripe
   d.zc_op.dsts.assign(size_t(rows), nullptr);
   d.zc_mode = std::max(0, std::min(2, knob(Knob::kPipeZc)));
-  d.d2h_per_shard = knob(Knob::kPipeD2hSplit) != 0;
   if (d.zc_mode && !(nsrc > 0 && rows > 0 && inline_ok(d.zc_op, size))) d.zc_mode = 0;
   if (nsrc > 0 && rows > 0) {
     for (int sl = 0; sl < depth; ++sl) {

@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 
 #include "gf_host.hpp"
 #include "matrix_host.hpp"
@@ -224,6 +226,61 @@ FusedOp PacketTracker::finish() const {
   return op;
 }
 
+namespace {
+// make_decoding_matrix with a process-wide cache: a read path decodes
+// stripe after stripe with one erasure pattern (a lost node), and the k x k
+// inversion is most of a small decode's host cost.  Keyed on
+// everything the result depends on -- k, m, w, the erased set and the whole
+// coding matrix, compared in full -- so a hit is the same inversion.
+struct DmEntry {
+  int k = 0, m = 0, w = 0, rc = 0;
+  std::vector<int> erased, matrix, dm, dm_ids;
+};
+
+int cached_decoding_matrix(int k, int m, int w, const int* matrix, const int* erased, int* dm, int* dm_ids) {
+  constexpr size_t kEntries = 1024;  // every 4-of-14 pattern of RS(10,4) fits (1,001); cleared when full
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, DmEntry> cache;
+  const size_t n = size_t(k) + size_t(m), km = size_t(k) * size_t(m), kk = size_t(k) * size_t(k);
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over the key
+  auto mix = [&h](int v) {
+    for (int b = 0; b < 4; ++b) h = (h ^ ((uint32_t(v) >> (8 * b)) & 0xFFu)) * 1099511628211ull;
+  };
+  mix(k);
+  mix(m);
+  mix(w);
+  for (size_t i = 0; i < n; ++i) mix(erased[i]);
+  for (size_t i = 0; i < km; ++i) mix(matrix[i]);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(h);
+    if (it != cache.end()) {
+      const DmEntry& e = it->second;
+      if (e.k == k && e.m == m && e.w == w && std::equal(e.erased.begin(), e.erased.end(), erased) &&
+          std::equal(e.matrix.begin(), e.matrix.end(), matrix)) {
+        std::copy(e.dm.begin(), e.dm.end(), dm);
+        std::copy(e.dm_ids.begin(), e.dm_ids.end(), dm_ids);
+        return e.rc;
+      }
+    }
+  }
+  DmEntry e;
+  e.k = k;
+  e.m = m;
+  e.w = w;
+  e.rc = make_decoding_matrix(k, m, w, matrix, erased, dm, dm_ids);
+  e.erased.assign(erased, erased + n);
+  e.matrix.assign(matrix, matrix + km);
+  e.dm.assign(dm, dm + kk);
+  e.dm_ids.assign(dm_ids, dm_ids + size_t(k));
+  const int rc = e.rc;
+  std::lock_guard<std::mutex> lk(mu);
+  if (cache.size() >= kEntries) cache.clear();
+  cache[h] = std::move(e);  // a colliding key replaces the entry (checked in full on every hit)
+  return rc;
+}
+}  // namespace
+
 void plan_encode(LinearTracker& t, int k, int m, const int* matrix, char** data, char** coding, int64_t size) {
   for (int i = 0; i < m; ++i) t.dotprod(k, matrix + i * k, nullptr, k + i, data, coding, size);
 }
@@ -244,7 +301,7 @@ int plan_decode(LinearTracker& t, int k, int m, const int* matrix, int row_k_one
   if (edd > 1 || (edd > 0 && (!row_k_ones || erased[k]))) {
     dm.resize(size_t(k) * k);
     dm_ids.resize(size_t(k));
-    if (make_decoding_matrix(k, m, t.w(), matrix, erased, dm.data(), dm_ids.data()) < 0) {
+    if (cached_decoding_matrix(k, m, t.w(), matrix, erased, dm.data(), dm_ids.data()) < 0) {
       std::free(erased);
       return -1;
     }

@@ -265,3 +265,41 @@ def test_handled_hip_error_does_not_leak_into_the_callers_hip_state_gpu(gpu):
     t = torch.full((4096,), 7, dtype=torch.uint8, device=gpu)
     torch.cuda.synchronize()
     assert int(t.sum()) == 7 * 4096
+
+
+def test_decode_matrix_cache_keys_on_the_whole_coding_matrix():
+    """The decoding-matrix cache (planner.cpp) must never serve one matrix's
+    inversion for another with the same erasure pattern: the same patterns
+    decoded under two coding matrices (the Vandermonde one and a copy with
+    its rows scaled), alternately, each on inconsistent inputs so the
+    survivor choice shows, against the compiled reference."""
+    _need_reference()
+    code = r'''
+import sys, os, ctypes, numpy as np
+sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
+from fallback_driver import LIB, REF, bind, ints, ptrs, matrix
+d = bind(os.path.join(LIB, "libjerasure_amd.so")); ref = bind(os.path.join(REF, "libjerasure_ref.so"))
+k, m, size = 6, 3, 4096
+A = matrix(d, k, m)
+B = [x if i < k else (x * 3) % 256 or 1 for i, x in enumerate(A)]  # rows 1.. differ
+rng = np.random.default_rng(9)
+# the two matrices decode the same inputs differently (else the test proves nothing)
+probe = [rng.integers(0, 256, size + 16, dtype=np.uint8) for _ in range(k + m)]
+pa, pb = [b.copy() for b in probe], [b.copy() for b in probe]
+ref["decode"](k, m, 8, ints(A), 0, ints([0, 1, 2, -1]), ptrs(pa[:k]), ptrs(pa[k:]), size)
+ref["decode"](k, m, 8, ints(B), 0, ints([0, 1, 2, -1]), ptrs(pb[:k]), ptrs(pb[k:]), size)
+assert any(not np.array_equal(a, b) for a, b in zip(pa, pb))
+bad = 0
+for it in range(40):
+    M = A if it % 2 == 0 else B
+    er = [[0, 1, 2], [1, 4, 7], [0, 6], [2, 5, 8]][(it // 2) % 4] + [-1]
+    bufs = [rng.integers(0, 256, size + 16, dtype=np.uint8) for _ in range(k + m)]  # inconsistent on purpose
+    mine = [b.copy() for b in bufs]
+    theirs = [b.copy() for b in bufs]
+    r1 = d["decode"](k, m, 8, ints(M), 0, ints(er), ptrs(mine[:k]), ptrs(mine[k:]), size)
+    r2 = ref["decode"](k, m, 8, ints(M), 0, ints(er), ptrs(theirs[:k]), ptrs(theirs[k:]), size)
+    bad += (r1 != r2) or any(not np.array_equal(a[:size], b[:size]) for a, b in zip(mine, theirs))
+print("bad", bad)
+'''
+    r = run_py(code, ECGPU_GPU=0)
+    assert r.returncode == 0 and "bad 0" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])

@@ -238,9 +238,13 @@ struct DmEntry {
 };
 
 int cached_decoding_matrix(int k, int m, int w, const int* matrix, const int* erased, int* dm, int* dm_ids) {
-  constexpr size_t kEntries = 1024;  // every 4-of-14 pattern of RS(10,4) fits (1,001); cleared when full
+  // bounded by entries (every 4-of-14 pattern of RS(10,4) fits: 1,001) and by
+  // the ints held (1 Mi = 4 MiB: a k = 255 inversion alone is 65,025), the
+  // whole cache cleared when either fills
+  constexpr size_t kEntries = 1024, kInts = size_t(1) << 20;
   static std::mutex mu;
   static std::unordered_map<uint64_t, DmEntry> cache;
+  static size_t held = 0;
   const size_t n = size_t(k) + size_t(m), km = size_t(k) * size_t(m), kk = size_t(k) * size_t(k);
   uint64_t h = 1469598103934665603ull;  // FNV-1a over the key
   auto mix = [&h](int v) {
@@ -274,9 +278,18 @@ int cached_decoding_matrix(int k, int m, int w, const int* matrix, const int* er
   e.dm.assign(dm, dm + kk);
   e.dm_ids.assign(dm_ids, dm_ids + size_t(k));
   const int rc = e.rc;
+  const size_t ints = e.erased.size() + e.matrix.size() + e.dm.size() + e.dm_ids.size();
+  if (ints > kInts / 16) return rc;  // too big to be worth holding
   std::lock_guard<std::mutex> lk(mu);
-  if (cache.size() >= kEntries) cache.clear();
-  cache[h] = std::move(e);  // a colliding key replaces the entry (checked in full on every hit)
+  if (cache.size() >= kEntries || held + ints > kInts) {
+    cache.clear();
+    held = 0;
+  }
+  auto it = cache.find(h);  // a colliding key replaces the entry (checked in full on every hit)
+  if (it != cache.end()) held -= it->second.erased.size() + it->second.matrix.size() + it->second.dm.size() +
+                                it->second.dm_ids.size();
+  held += ints;
+  cache[h] = std::move(e);
   return rc;
 }
 }  // namespace

@@ -163,10 +163,11 @@ class EcgpuError(RuntimeError):
 # fails loudly instead (EcgpuError), so no checked or measured result can come
 # from the CPU.  An ECGPU_CPU_FALLBACK set in the environment wins.
 #
-# ECGPU_MIN_OFFLOAD_KIB: the C library runs small host-memory calls on its CPU
-# executor (below the measured crossover); this package sends
-# every call to the GPU, so each checked or measured result is the HIP path's.
-PACKAGE_KNOB_DEFAULTS = {"ECGPU_CPU_FALLBACK": 0, "ECGPU_MIN_OFFLOAD_KIB": 0}
+# ECGPU_MIN_OFFLOAD_KIB / ECGPU_LINK_CALLS: the C library runs small
+# host-memory calls, and large ones arriving while another holds the device's
+# link, on its CPU executor; this package sends every call to
+# the GPU, so each checked or measured result is the HIP path's.
+PACKAGE_KNOB_DEFAULTS = {"ECGPU_CPU_FALLBACK": 0, "ECGPU_MIN_OFFLOAD_KIB": 0, "ECGPU_LINK_CALLS": 0}
 
 
 def _apply_package_defaults(names=None) -> None:

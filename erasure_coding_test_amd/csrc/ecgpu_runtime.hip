@@ -1106,6 +1106,36 @@ int64_t bytes_moved(const FusedOp& op, int64_t size) {
   return int64_t(n) * size;
 }
 
+// Host-memory synchronous calls in flight on each device's link (the PCIe
+// link a staged or zero-copy call moves its bytes over).  One such call
+// already runs the link at its ceiling (2 concurrent C3 4 MiB pageable
+// encodes: 36.0 GiB/s together against 34.3 alone), so with ECGPU_LINK_CALLS
+// (default 1) calls in flight, a further one runs on the CPU executor on its
+// own thread instead of queueing for the link: concurrent
+// callers then add cores rather than wait.
+constexpr int kLinkSlots = 64;
+std::atomic<int> g_link_calls[kLinkSlots];
+
+struct LinkScope {
+  int slot = -1;
+  LinkScope(int device, bool host_io) {
+    if (host_io && device >= 0) {
+      slot = device % kLinkSlots;
+      g_link_calls[slot].fetch_add(1, std::memory_order_relaxed);
+    }
+  }
+  ~LinkScope() {
+    if (slot >= 0) g_link_calls[slot].fetch_sub(1, std::memory_order_relaxed);
+  }
+  LinkScope(const LinkScope&) = delete;
+  LinkScope& operator=(const LinkScope&) = delete;
+};
+
+bool link_busy(int device) {
+  const int limit = knob(Knob::kLinkCalls);
+  return limit > 0 && device >= 0 && g_link_calls[device % kLinkSlots].load(std::memory_order_relaxed) >= limit;
+}
+
 // A synchronous call over `size` bytes of every buffer of the fused op.
 int execute(const FusedOp& op, int64_t size, const char* call) {
   if (op.w != 8 && size % (op.w / 8) != 0)
@@ -1117,7 +1147,8 @@ int execute(const FusedOp& op, int64_t size, const char* call) {
   // small host-memory calls (and all of them with ECGPU_GPU=0) on the CPU
   // executor: below the crossover the GPU round trip costs more than the
   // arithmetic (cpu_fallback.hpp)
-  if (cpu_by_choice(bytes_moved(op, size)) && all_host(op)) {
+  const bool host = all_host(op);
+  if (host && cpu_by_choice(bytes_moved(op, size))) {
     record_cpu_call();
     cpu_apply(op, size);
     return ECGPU_OK;
@@ -1125,7 +1156,14 @@ int execute(const FusedOp& op, int64_t size, const char* call) {
   int ndev = 1;
   const int ways = split_ways(op, size, &ndev);
   if (ways > 1) return execute_split(op, size, ways, ndev, call);
-  return execute_on(op, size, call_device(op.srcs, op.dsts), call);
+  const int device = call_device(op.srcs, op.dsts);
+  if (host && link_busy(device)) {  // the link is taken: this caller's core does the work
+    record_cpu_call();
+    cpu_apply(op, size);
+    return ECGPU_OK;
+  }
+  LinkScope link(device, host);
+  return execute_on(op, size, device, call);
 }
 
 ECGPU_RT_END

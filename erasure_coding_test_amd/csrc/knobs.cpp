@@ -61,6 +61,7 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_PIPE_ZC", "pipe_zc", 0},
     {"ECGPU_PIPE_CONTIG", "pipe_contig", 1},
     {"ECGPU_PIPE_FLAT", "pipe_flat", 1},
+    {"ECGPU_LINK_CALLS", "link_calls", 1},
 };
 
 constexpr int kUnset = INT_MIN;

@@ -61,6 +61,8 @@ enum class Knob : int {
   kPipeFlat,        // ECGPU_PIPE_FLAT: runs contiguous on both sides move as one 1-D copy (copy_shards); 0 = as a
                     // 2-D copy anyway (HIP's 2-D device->pinned copy: +4 % for one process, collapsing when
                     // processes share the GPU)
+  kLinkCalls,       // ECGPU_LINK_CALLS: host-memory synchronous calls allowed in flight on one device's link before
+                    // a further one runs on the CPU executor (0 = no limit)
   kCount
 };
 

@@ -39,7 +39,8 @@ def _need_reference():
 
 def _env(**kw):
     env = {k: v for k, v in os.environ.items()
-           if k not in ("ECGPU_GPU", "EC_GPU", "ECGPU_MIN_OFFLOAD_KIB", "ECGPU_CPU_SIMD", "ECGPU_TEST_INJECT_HIP")}
+           if k not in ("ECGPU_GPU", "EC_GPU", "ECGPU_MIN_OFFLOAD_KIB", "ECGPU_CPU_SIMD", "ECGPU_TEST_INJECT_HIP",
+                        "ECGPU_LINK_CALLS")}
     env["ECGPU_CPU_FALLBACK"] = "0"  # nothing may reach the CPU through the fallback here
     env.update({k: str(v) for k, v in kw.items()})
     return env
@@ -303,3 +304,51 @@ print("bad", bad)
 '''
     r = run_py(code, ECGPU_GPU=0)
     assert r.returncode == 0 and "bad 0" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
+@pytest.mark.gpu
+def test_link_busy_calls_run_on_the_cpu_bit_exact_gpu():
+    """ECGPU_LINK_CALLS (the C library's default 1): a large host-memory call
+    arriving while another holds the device's link runs on the CPU executor.
+    Four threads encode their own pageable RS(10,4) 4 MiB stripes through the
+    mangled names at once (the small-call threshold at 0, so only the link
+    rule routes); some calls take the CPU, and every parity equals the same
+    stripe's parity computed with every call on the GPU."""
+    code = r'''
+import os, sys, ctypes, threading, numpy as np
+sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
+from fallback_driver import LIB, bind, ints, ptrs, matrix
+d = bind(os.path.join(LIB, "libjerasure_amd.so"))
+core = ctypes.CDLL(os.path.join(LIB, "libecgpu.so"))
+core.ecgpu_set_knob.argtypes = [ctypes.c_char_p, ctypes.c_int]
+core.ecgpu_cpu_call_count.restype = ctypes.c_int64
+k, m, S = 10, 4, 4 << 20
+M = matrix(d, k, m)
+core.ecgpu_set_knob(b"ECGPU_MIN_OFFLOAD_KIB", 0)
+rng = np.random.default_rng(5)
+stripes = [[rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] for _ in range(4)]
+core.ecgpu_set_knob(b"ECGPU_LINK_CALLS", 0)  # reference parities: every call on the GPU
+want = []
+for st in stripes:
+    c = [np.zeros(S, np.uint8) for _ in range(m)]
+    d["encode"](k, m, 8, ints(M), ptrs(st), ptrs(c), S)
+    want.append(c)
+before = core.ecgpu_cpu_call_count()
+core.ecgpu_set_knob(b"ECGPU_LINK_CALLS", 1)
+bad = []
+def worker(i):
+    for rep in range(6):
+        c = [np.full(S, 0x5A, np.uint8) for _ in range(m)]
+        d["encode"](k, m, 8, ints(M), ptrs(stripes[i]), ptrs(c), S)
+        if any(not np.array_equal(a, b) for a, b in zip(c, want[i])):
+            bad.append((i, rep))
+ts = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+[t.start() for t in ts]
+[t.join() for t in ts]
+print("bad", len(bad), "cpu_calls", core.ecgpu_cpu_call_count() - before)
+'''
+    r = run_py(code)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    words = r.stdout.split()
+    assert words[words.index("bad") + 1] == "0", r.stdout
+    assert 0 < int(words[words.index("cpu_calls") + 1]) < 24, r.stdout

@@ -1147,8 +1147,10 @@ int execute(const FusedOp& op, int64_t size, const char* call) {
   // small host-memory calls (and all of them with ECGPU_GPU=0) on the CPU
   // executor: below the crossover the GPU round trip costs more than the
   // arithmetic (cpu_fallback.hpp)
-  const bool host = all_host(op);
-  if (host && cpu_by_choice(bytes_moved(op, size))) {
+  // (pointer classification costs ~0.15 us a buffer: only when a rule needs it)
+  const bool small = cpu_by_choice(bytes_moved(op, size));
+  const bool host = (small || knob(Knob::kLinkCalls) > 0) && all_host(op);
+  if (small && host) {
     record_cpu_call();
     cpu_apply(op, size);
     return ECGPU_OK;

@@ -62,7 +62,6 @@ constexpr KnobDef kDefs[int(Knob::kCount)] = {
     {"ECGPU_PIPE_CONTIG", "pipe_contig", 1},
     {"ECGPU_PIPE_FLAT", "pipe_flat", 1},
     {"ECGPU_LINK_CALLS", "link_calls", 1},
-    {"ECGPU_PIPE_D2H_GRID", "pipe_d2h_grid", 0},
 };
 
 constexpr int kUnset = INT_MIN;

@@ -63,8 +63,6 @@ enum class Knob : int {
                     // processes share the GPU)
   kLinkCalls,       // ECGPU_LINK_CALLS: host-memory synchronous calls allowed in flight on one device's link before
                     // a further one runs on the CPU executor (0 = no limit)
-  kPipeD2hGrid,     // ECGPU_PIPE_D2H_GRID: host pipelines copy outputs back to pinned buffers with their own kernel
-                    // of this many workgroups (0 = HIP's D2H copy; read at creation)
   kCount
 };
 

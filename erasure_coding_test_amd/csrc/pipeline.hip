@@ -32,32 +32,6 @@ using namespace ecgpu;
 using namespace ecgpu::rt;
 
 namespace {
-// ECGPU_PIPE_D2H_GRID > 0 (an A/B experiment): a slot's outputs copied back
-// by this kernel -- `grid` workgroups, grid-stride over 16-B columns of each
-// shard, non-temporal HBM loads, stores straight into the pinned host
-// buffers through their device mapping -- instead of HIP's D2H blit.
-struct D2hArgs {
-  const uint8_t* src[8];
-  uint8_t* dst[8];
-  int n;
-  int64_t size;
-};
-
-typedef uint32_t d2h_u32x4 __attribute__((ext_vector_type(4)));
-
-__global__ __launch_bounds__(256) void d2h_copy(D2hArgs a) {
-  const int64_t nvec = a.size / 16;
-  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  for (int r = 0; r < a.n; ++r) {
-    const d2h_u32x4* s = reinterpret_cast<const d2h_u32x4*>(a.src[r]);
-    d2h_u32x4* d = reinterpret_cast<d2h_u32x4*>(a.dst[r]);
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec; i += stride)
-      d[i] = __builtin_nontemporal_load(s + i);
-    for (int64_t i = nvec * 16 + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < a.size; i += stride)
-      a.dst[r][i] = a.src[r][i];
-  }
-}
-
 // The HIP side of a host pipeline (hostsync::StripePipeline's Ops): a ring
 // of `depth` device stripe slots, one bound plan per slot, three streams and
 // per-slot loaded / computed / drained events.
@@ -74,7 +48,6 @@ struct PipeDevice {
   // pinned host buffers in place, 2 it also reads the sources there (no DMA);
   // a stripe whose buffers are not all mapped host memory takes the DMA path.
   int zc_mode = 0;
-  int d2h_grid = 0;                   // ECGPU_PIPE_D2H_GRID (read at creation): see d2h_copy
   FusedOp zc_op;                      // the map for gf_apply_inl launches (coef only; pointers per stripe)
   std::vector<char> zc_slot;          // per slot: its outputs were written in place (no D2H)
 
@@ -161,26 +134,7 @@ struct PipeDevice {
   // D2H of a slot's outputs (s_d2h, after the slot's compute), then drained.
   int d2h(int sl, const std::vector<char*>& hp) {
     ECGPU_HIP(hipStreamWaitEvent(s_d2h, computed[sl], 0));
-    bool copied = zc_slot[size_t(sl)] != 0;  // (written in place by the kernel: nothing to copy)
-    if (!copied && d2h_grid > 0 && hp.size() <= 8 && size % 16 == 0) {
-      D2hArgs a{};
-      bool mapped = true;
-      for (size_t i = 0; i < hp.size() && mapped; ++i) {
-        void* dv = nullptr;
-        mapped = host_mapped(hp[i], size_t(size), &dv) && (reinterpret_cast<uintptr_t>(dv) & 15u) == 0;
-        a.src[i] = slot_shard(sl, nsrc() + int(i));
-        a.dst[i] = static_cast<uint8_t*>(dv);
-      }
-      if (mapped) {
-        a.n = int(hp.size());
-        a.size = size;
-        void* args[] = {&a};
-        ECGPU_HIP(hipLaunchKernel(reinterpret_cast<const void*>(&d2h_copy), dim3(unsigned(d2h_grid)), dim3(256), args,
-                                  0, s_d2h));
-        copied = true;
-      }
-    }
-    if (!copied)
+    if (!zc_slot[size_t(sl)])  // (written in place by the kernel: nothing to copy)
       if (int rc = copy_shards(false, slot_shard(sl, nsrc()), slot_stride, hp, size_t(size), s_d2h)) return rc;
     ECGPU_HIP(hipEventRecord(drained[sl], s_d2h));
     return ECGPU_OK;
@@ -269,7 +223,6 @@ ecgpu_pipeline* pipeline_build(int k, int m, int rows, int nsrc, const int* coef
   d.zc_op.srcs.assign(size_t(nsrc), nullptr);  // counts only (inline_ok); pointers are per stripe
   d.zc_op.dsts.assign(size_t(rows), nullptr);
   d.zc_mode = std::max(0, std::min(2, knob(Knob::kPipeZc)));
-  d.d2h_grid = std::max(0, knob(Knob::kPipeD2hGrid));
   if (d.zc_mode && !(nsrc > 0 && rows > 0 && inline_ok(d.zc_op, size))) d.zc_mode = 0;
   if (nsrc > 0 && rows > 0) {
     for (int sl = 0; sl < depth; ++sl) {

@@ -12,3 +12,4 @@ g++ -O2 -Wall -std=c++17 tools/crossover.cpp -Iinclude/dropin -Lerasure_coding_t
 /opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/hip_overheads.cpp -o tools/hip_overheads.bin -lpthread
 /opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/zero_copy_probe.cpp -o tools/zero_copy_probe.bin
 /opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/pageable_duplex_probe.cpp -o tools/pageable_duplex_probe.bin -lpthread
+/opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/sdma_d2h_probe.cpp -lhsa-runtime64 -o tools/sdma_d2h_probe.bin

@@ -164,6 +164,10 @@ def test_bench_gpus2_rehearsal_spawns_two_ranks(gpu):
     roof = d["roofline"]
     assert roof["frac"] > 0 and len(roof["frac_per_rank"]) == 2
     assert roof["frac_worst_rank"] == min(roof["frac_per_rank"])
+    # the contract's achieved: algorithmic bytes / the AVERAGE timed launch (round 6)
+    want = roof["algorithmic_bytes_per_launch"] / (roof["mean_launch_ms"] / 1e3) / 1e9 / roof["peak"]
+    assert abs(roof["frac"] - want) < 2e-3, (roof["frac"], want)
+    assert roof["mean_launch_ms"] > 0 and roof["median_launch_ms"] > 0
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] == 1
     assert d["selfcheck_vs_reference_cpu"] is True
     for p in d["per_rank"]:

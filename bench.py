@@ -1076,6 +1076,7 @@ def main(argv=None):
     enc_frac = enc_bytes / (enc_mean_ms / 1e3) / 1e9 / HBM_PEAK_GBS
     mine = {"rank": rank, "device": local, **device_identity(N, local), "elapsed_s": round(elapsed, 6),
             "encode_mean_ms": round(enc_mean_ms, 4), "encode_median_ms": round(enc_ms, 4),
+            "encode_launch_ms": [round(x, 4) for x in enc_times],  # in step order: the DVFS recovery shows here
             "encode_frac": round(enc_frac, 4),
             "decode_median_ms": round(dec_ms, 4) if dec_ms is not None else None,
             "decode_frac": (round(dec_bytes / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if dec_ms is not None
